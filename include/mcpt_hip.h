@@ -1,0 +1,230 @@
+/*
+ * mcpt_hip.h — C ABI of the MI355X path-tracing hot path (libmcpt_hip.so).
+ *
+ * The reference drives its per-sample loop through C++ module interfaces
+ * (MonteCarloPathTracing/ is abbreviated MCPT/ below):
+ *   RayGeneration::init/generateRay        MCPT/raygeneration.h:15-17, raygeneration.cpp:29-67
+ *   SceneBuild::buildScene/init            MCPT/scenebuild.h:31-33,   scenebuild.cpp:50-101,149-169
+ *   SceneBase::intersect/shade             MCPT/scenebuild.h:15-16,   scenebuild.cpp:103-145
+ *   ColorOut::init/outputColorCL           MCPT/colorout.h:6-8,       colorout.cpp:31-73
+ *   OpenCL::init/update (the frame loop)   MCPT/OpenCLApp.h:4-5,      OpenCLApp.cpp:36-82
+ *   ThirdPartyWrapper::loadObject/outputPicture  MCPT/thirdpartywrapper.h:13-16
+ *   Auxiliary::parseCamera                 MCPT/auxiliary.h:27,       auxiliary.cpp:20-71
+ *   BVH::HLBVH<CPU>                        MCPT/BVH/hlbvh.h:10-26,    hlbvh.cpp:92-200
+ * Every entry point below names the interface it replaces.
+ *
+ * Conventions
+ *  - Plain C: POD structs, pointers + sizes, int status (0 = MCPT_OK, < 0 =
+ *    error), no exceptions cross the boundary; mcpt_last_error() explains the
+ *    last failure of the calling thread.
+ *  - Record structs are byte-identical to MCPT/objdef.h:21-99 (Camera 80 B,
+ *    Ray 48 B, Hit 48 B, Triangle 64 B, Material 48 B, BVHNode 64 B), so a
+ *    reference host can hand its own vectors over unchanged.
+ *  - "_dev" pointers are device (HBM) pointers, "stream" is a hipStream_t
+ *    passed as void* (NULL = default stream).  Host pointers are never
+ *    retained after a call returns.
+ *  - A context is bound to one GPU and is not thread-safe: one host thread or
+ *    process per GPU (multi-GPU = one process per GPU).
+ */
+#ifndef MCPT_HIP_H
+#define MCPT_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---------------------------------------------------------------- status */
+#define MCPT_OK 0
+#define MCPT_ERR_ARG (-1)      /* bad argument / size mismatch              */
+#define MCPT_ERR_HIP (-2)      /* HIP runtime failure                        */
+#define MCPT_ERR_IO (-3)       /* file could not be read / written           */
+#define MCPT_ERR_PARSE (-4)    /* malformed OBJ / MTL / JSON                 */
+#define MCPT_ERR_LIMIT (-5)    /* BVH deeper than the reference's stack[64]  */
+#define MCPT_ERR_NOGPU (-6)    /* no HIP device / device index out of range  */
+
+/* ------------------------------------------------------ records (objdef.h) */
+typedef struct mcpt_camera {        /* objdef.h:21-27, 80 B */
+  float center[4], direction[4], up[4], horizontal[4];
+  float arg;                        /* vertical fov in radians              */
+  float tmin;
+  uint32_t camera_type;             /* 0 perspective, 1 orthographic        */
+  float pad;
+} mcpt_camera;
+
+typedef struct mcpt_ray {           /* objdef.h:29-39, 48 B */
+  float origin[4];                  /* .w bits: int term_depth              */
+  float direction[4];               /* .w bits: int pixel id                */
+  float ratio[4];                   /* unused by the reference              */
+} mcpt_ray;
+
+typedef struct mcpt_hit {           /* objdef.h:41-48, 48 B */
+  float normal[4];
+  float point[4];
+  float t;                          /* FLT_MAX = miss                       */
+  uint32_t triangle_id;
+  uint32_t material_id;
+  uint32_t pad;
+} mcpt_hit;
+
+typedef struct mcpt_triangle {      /* objdef.h:50-56, 64 B */
+  float v[3][4];
+  float normal[4];                  /* .w bits: int material id             */
+} mcpt_triangle;
+
+enum {                              /* objdef.h:58-67 */
+  MCPT_DIFFUSE = 1,
+  MCPT_GLOSSY = 2,
+  MCPT_TRANSPARENT = 3,
+  MCPT_LIGHT = 4
+};
+
+typedef struct mcpt_material {      /* objdef.h:69-79, 48 B */
+  int32_t type;
+  float Ni, Ns, pad;
+  float kd[4];
+  float ka_ks[4];                   /* ka for LIGHT, ks for GLOSSY          */
+} mcpt_material;
+
+typedef struct mcpt_bvh_node {      /* objdef.h:91-99, 64 B */
+  float bbmin[4], bbmax[4], pad[4];
+  int32_t parent, left, right, pad2;/* leaf: left == right == triangle id   */
+} mcpt_bvh_node;
+
+/* ray.origin.w / term_depth bitfield (shade.cl:100-206) */
+#define MCPT_TERMINATED 0xFF000000u
+#define MCPT_INSIDE     0x00FF0000u
+#define MCPT_DEPTH_MASK 0x0000FFFFu
+
+/* -------------------------------------------------------- opaque handles */
+typedef struct mcpt_ctx mcpt_ctx;
+typedef struct mcpt_scene mcpt_scene;
+
+/* Render modes for the fused path.
+ *  MCPT_MODE_EXACT   — reference arithmetic, traversal order and tie rule;
+ *                      closest-hit pruning only where it cannot change the
+ *                      accepted hit.  The default.
+ *  MCPT_MODE_NOPRUNE — exhaustive left-first traversal exactly as
+ *                      objdef.h:240-275 (slow; parity cross-check).          */
+#define MCPT_MODE_EXACT   0
+#define MCPT_MODE_NOPRUNE 1
+
+typedef struct mcpt_render_params {
+  int32_t width, height;            /* config width/height (= camera.resolution) */
+  int32_t max_depth;                /* config "maxdepth"  (-D MAX_DEPTH)   */
+  int32_t max_attempt;              /* config "attempt"   (-D MAX_ATTEMPT) */
+  int32_t frame_begin;              /* first frame index of this call (attemptCount) */
+  int32_t frames;                   /* frames to render in this call       */
+  int32_t stripe_rows;              /* multi-GPU tile: rows per stripe      */
+  int32_t stripe_index;             /* this GPU's stripe residue            */
+  int32_t stripe_count;             /* number of GPUs (1 = whole image)     */
+  int32_t mode;                     /* MCPT_MODE_*                          */
+  int32_t frames_per_launch;        /* 0 = auto                             */
+  int32_t reserved;
+} mcpt_render_params;
+
+typedef struct mcpt_stats {
+  uint64_t segments;                /* rays alive at intersect entry, all frames */
+  uint64_t node_visits;             /* BVH nodes whose children were tested */
+  uint64_t tri_tests;               /* triangle tests                        */
+  uint64_t bad_material;            /* hits on an unknown material type      */
+  double   kernel_ms;               /* device time of the last render call   */
+  int32_t  launches;                /* kernel launches of the last render call */
+  int32_t  pad;
+} mcpt_stats;
+
+/* ------------------------------------------------------- version / errors */
+const char *mcpt_version(void);
+const char *mcpt_last_error(void);
+
+/* ----------------------------------------------------------- host side
+ * Everything here is plain C++ on the host; no GPU needed.               */
+
+/* Auxiliary::parseCamera (auxiliary.cpp:20-71): JSON camera -> Camera.   */
+int mcpt_parse_camera(const double position[3], const double lookat[3],
+                      const double up[3], double fov_deg, mcpt_camera *out);
+
+/* MTL record -> Material, thirdpartywrapper.cpp:65-97 precedence:
+ * ior != 1 -> TRANSPARENT; any Ka > 0 -> LIGHT; Ns != 1 -> GLOSSY; else DIFFUSE. */
+int mcpt_classify_material(float ior, const float ambient[3], const float diffuse[3],
+                           const float specular[3], float shininess, mcpt_material *out);
+
+/* ThirdPartyWrapper::loadObject (thirdpartywrapper.cpp:25-99) on an
+ * OBJ + its MTL library: two-call pattern — call with NULL outputs to get
+ * the counts, then again with arrays of that size.  Triangles come out
+ * with v[] filled and normal zeroed (SceneCL packs them, below);
+ * mat_index[i] is the per-face material index (-1 if none).            */
+int mcpt_load_obj(const char *directory, const char *objname,
+                  mcpt_triangle *tris, int32_t *mat_index, int64_t *n_tris,
+                  mcpt_material *mats, int32_t *n_mats);
+
+/* SceneCL ctor packing (scenebuild.cpp:58-62): normal = normalize(cross(
+ * v1-v0, v2-v0)), normal.w <- material index bits.  In place.           */
+int mcpt_pack_triangles(mcpt_triangle *tris, const int32_t *mat_index, int64_t n);
+
+/* HLBVH<CPU>::build (hlbvh.cpp:92-200): Morton LBVH, 2n-1 nodes, root 0,
+ * leaves at [n-1, 2n-2].  nodes must hold 2n-1 records.                 */
+int mcpt_build_hlbvh(const mcpt_triangle *tris, int64_t n, mcpt_bvh_node *nodes);
+
+/* Max DFS stack depth the reference traversal needs on this tree.      */
+int mcpt_bvh_stack_depth(const mcpt_bvh_node *nodes, int64_t n_nodes, int32_t *depth);
+
+/* ThirdPartyWrapper::outputPicture (thirdpartywrapper.cpp:14-23):
+ * stbi_write_hdr with vertical flip, 4 components in, RGB out.           */
+int mcpt_write_hdr(const char *path, int32_t width, int32_t height,
+                   const float *rgba, int32_t flip_vertically);
+/* Same encoder into memory: returns the byte count (call with NULL first). */
+int64_t mcpt_encode_hdr(int32_t width, int32_t height, const float *rgba,
+                        int32_t flip_vertically, uint8_t *out, int64_t cap);
+
+/* ---------------------------------------------------------- device side */
+
+/* OpenCLBasic::init (oclbasic.cpp:75-122) equivalent: bind to a GPU.     */
+int mcpt_ctx_create(int32_t device, mcpt_ctx **out);
+int mcpt_ctx_destroy(mcpt_ctx *ctx);
+int mcpt_device_count(int32_t *count);
+
+/* SceneBuild::buildScene (scenebuild.cpp:50-101,149-156): upload the packed
+ * triangles + reference BVH + materials; converted to the device layout
+ * (child-box nodes, Cramer-ready triangles — DESIGN.md §2) once here.   */
+int mcpt_scene_upload(mcpt_ctx *ctx, const mcpt_triangle *tris, int64_t n_tris,
+                      const mcpt_bvh_node *nodes, int64_t n_nodes,
+                      const mcpt_material *mats, int32_t n_mats, mcpt_scene **out);
+int mcpt_scene_destroy(mcpt_scene *scene);
+
+/* Fused per-pixel path loop: for every pixel of this GPU's stripes and
+ * frames [frame_begin, frame_begin+frames): generateRay -> maxdepth x
+ * (intersect, shade) -> history accumulate, exactly the per-pixel effect of
+ * OpenCL::update (OpenCLApp.cpp:57-82) + ColorOut (colorout.cpp:40-73).
+ * seeds/hist/count are W*H device arrays (u32, float4, i32) that persist
+ * across calls; pixels outside this GPU's stripes are left untouched.    */
+int mcpt_render_frames(mcpt_ctx *ctx, const mcpt_scene *scene, const mcpt_camera *cam,
+                       const mcpt_render_params *params, uint32_t *seeds_dev,
+                       float *hist_dev, int32_t *count_dev, void *stream);
+
+/* Wavefront kernels on the reference's AoS records, one per reference
+ * kernel, for drop-in use and kernel-level parity:                       */
+/* rayGenerator.cl generateRay (W x H NDRange)                            */
+int mcpt_generate_rays(mcpt_ctx *ctx, const mcpt_camera *cam, int32_t width, int32_t height,
+                       mcpt_ray *rays_dev, void *stream);
+/* intersect.cl intersectRays (tmin = EPSILON 1e-3, oclbasic.h:193)        */
+int mcpt_intersect(mcpt_ctx *ctx, const mcpt_scene *scene, const mcpt_ray *rays_dev,
+                   int64_t n, mcpt_hit *hits_dev, float tmin, int32_t mode, void *stream);
+/* shade.cl shade (-D MAX_DEPTH)                                           */
+int mcpt_shade(mcpt_ctx *ctx, const mcpt_scene *scene, mcpt_ray *rays_dev,
+               const mcpt_hit *hits_dev, float *color_dev, uint32_t *seeds_dev, int64_t n,
+               int32_t max_depth, void *stream);
+/* history.cl func (-D MAX_ATTEMPT): running mean of non-zero samples      */
+int mcpt_accumulate(mcpt_ctx *ctx, float *color_dev, float *hist_dev, int32_t *count_dev,
+                    int64_t n, int32_t max_attempt, void *stream);
+
+/* Counters of the last render call (segments etc. need stats enabled).   */
+int mcpt_set_stats(mcpt_ctx *ctx, int32_t enabled);
+int mcpt_get_stats(mcpt_ctx *ctx, mcpt_stats *out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MCPT_HIP_H */

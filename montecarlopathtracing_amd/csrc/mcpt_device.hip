@@ -1,0 +1,787 @@
+// mcpt_device.hip — device half of libmcpt_hip.so: the per-pixel, per-sample
+// path-tracing loop for gfx950 (MI355X), behind the C ABI of include/mcpt_hip.h.
+//
+// Reference kernels restated here (arithmetic in mcpt_refmath.h):
+//   generateRay     MCPT/kernels/rayGenerator.cl:1-31
+//   intersectRays   MCPT/kernels/intersect.cl:1-28 + MCPT/objdef.h:178-275
+//   shade           MCPT/kernels/shade.cl:75-206
+//   func (history)  MCPT/kernels/history.cl:3-28
+//   frame loop      MCPT/OpenCLApp.cpp:57-82, MCPT/colorout.cpp:40-73
+//
+// Two ways to run them:
+//  * k_render — the fused path: one lane per pixel, the lane walks all of its
+//    frames itself (seed chain, running mean and count stay in registers,
+//    path regeneration on termination), BVH stack in LDS.  This is the hot
+//    path measured by bench.py.
+//  * k_generate / k_intersect / k_shade / k_accumulate — one kernel per
+//    reference kernel on the reference's AoS records, for drop-in use and for
+//    kernel-level parity with the reference code objects.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/mcpt_hip.h"
+#include "mcpt_refmath.h"
+
+using namespace mcpt;
+
+namespace mcpt {
+int fail(int code, const std::string &msg);  // mcpt_host.cpp
+}
+
+// ------------------------------------------------------------ device layout
+// Internal node n of the reference HLBVH keeps its index; its record stores
+// BOTH children's boxes so one 64-B fetch decides where to go next
+// (objdef.h:252-273 fetches and tests one 64-B node per step).
+struct __attribute__((aligned(16))) DevNode {
+  f4 a;  // Lmin.x Lmin.y Lmin.z Lmax.x
+  f4 b;  // Lmax.y Lmax.z Rmin.x Rmin.y
+  f4 c;  // Rmin.z Rmax.x Rmax.y Rmax.z
+  int32_t left, right, pad0, pad1;  // >= 0 internal node, < 0 leaf: ~triangle
+};
+// Cramer-ready triangle: v0, -(v1-v0), -(v2-v0) exactly as objdef.h:190-199
+// forms them, plus the packed normal (.w = material id bits).
+struct __attribute__((aligned(16))) DevTri {
+  f4 v0;
+  f4 nab;
+  f4 nac;
+  f4 nrm;
+};
+static_assert(sizeof(DevNode) == 64 && sizeof(DevTri) == 64, "64-B records");
+
+struct SceneView {
+  const DevNode *nodes;
+  const DevTri *tris;
+  const mcpt_material *mats;
+  f4 root_min, root_max;
+  int32_t root_leaf;  // >= 0: single-triangle scene, root is that leaf
+  int32_t n_mats;
+  float prune_margin;
+};
+
+struct mcpt_scene {
+  int device;
+  DevNode *nodes = nullptr;
+  DevTri *tris = nullptr;
+  mcpt_material *mats = nullptr;
+  int64_t n_tris = 0, n_internal = 0;
+  int32_t n_mats = 0;
+  int32_t stack_depth = 1;
+  SceneView view;
+};
+
+struct mcpt_ctx {
+  int device;
+  bool stats_on = false;
+  unsigned long long *d_stats = nullptr;  // segments, nodes, tris, bad
+  mcpt_stats last;
+  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+};
+
+#define HIP_OK(expr)                                                                        \
+  do {                                                                                      \
+    hipError_t e_ = (expr);                                                                 \
+    if (e_ != hipSuccess) return mcpt::fail(MCPT_ERR_HIP, std::string(#expr) + ": " + hipGetErrorString(e_)); \
+  } while (0)
+
+// ----------------------------------------------------------------- traversal
+struct Trace {
+  float t;        // closest accepted t (FLT_MAX = miss)
+  int32_t tri;    // triangle that set t
+  int32_t last;   // last accepted triangle (the reference's Hit.triangleID)
+  uint32_t nodes, tests;
+};
+
+template <bool LITERAL>
+__device__ inline BoxT box_test(f3 bmin, f3 bmax, f3 o, f3 d, f3 rinv) {
+  if (LITERAL) {  // objdef.h:227-228 verbatim: (bb - o) / d
+    f3 t1 = (bmin - o) / d;
+    f3 t2 = (bmax - o) / d;
+    BoxT r;
+    r.tnear = fmaxf(fmaxf(fminf(t1.x, t2.x), fminf(t1.y, t2.y)), fminf(t1.z, t2.z));
+    r.tfar = fminf(fminf(fmaxf(t1.x, t2.x), fmaxf(t1.y, t2.y)), fmaxf(t1.z, t2.z));
+    return r;
+  }
+  return slab(bmin, bmax, o, rinv);
+}
+
+__device__ inline void test_tri(const DevTri *__restrict__ tris, int32_t id, f3 o, f3 d, float tmin,
+                                Trace &tr) {
+  const DevTri T = tris[id];
+  TriHit h = cramer(d, T.nab.xyz, T.nac.xyz, T.v0.xyz - o, T.nrm.xyz, tmin);
+  tr.tests++;
+  if (h.accept) {
+    tr.last = id;
+    if (tr.t - h.t >= kEps) {  // objdef.h:213 — first-found wins near-ties
+      tr.t = h.t;
+      tr.tri = id;
+    }
+  }
+}
+
+// Left-first DFS of objdef.h:240-275.  PRUNE skips a child whose box starts
+// farther than the current hit plus a margin: every triangle inside it would
+// have t > hit.t and could not replace the hit.
+template <bool PRUNE, bool LITERAL>
+__device__ inline Trace traverse(const SceneView &S, f3 o, f3 d, float tmin, int32_t *stk, int stride) {
+  Trace tr;
+  tr.t = kFltMax;
+  tr.tri = -1;
+  tr.last = -1;
+  tr.nodes = 0;
+  tr.tests = 0;
+  f3 rinv;
+  rinv.x = __builtin_amdgcn_rcpf(d.x);
+  rinv.y = __builtin_amdgcn_rcpf(d.y);
+  rinv.z = __builtin_amdgcn_rcpf(d.z);
+  if (!slab_pass(box_test<LITERAL>(S.root_min.xyz, S.root_max.xyz, o, d, rinv), tmin)) return tr;
+  if (S.root_leaf >= 0) {
+    test_tri(S.tris, S.root_leaf, o, d, tmin, tr);
+    return tr;
+  }
+  const DevNode *__restrict__ nodes = S.nodes;
+  int32_t node = 0;
+  int sp = 0;
+  for (;;) {
+    const DevNode N = nodes[node];
+    tr.nodes++;
+    f3 lmin = N.a.xyz, lmax = (f3){N.a.w, N.b.x, N.b.y};
+    f3 rmin = (f3){N.b.z, N.b.w, N.c.x}, rmax = N.c.yzw;
+    BoxT bl = box_test<LITERAL>(lmin, lmax, o, d, rinv);
+    BoxT br = box_test<LITERAL>(rmin, rmax, o, d, rinv);
+    bool hl = slab_pass(bl, tmin), hr = slab_pass(br, tmin);
+    if (PRUNE) {
+      const float lim = tr.t + S.prune_margin;
+      hl = hl && !(bl.tnear > lim);
+      hr = hr && !(br.tnear > lim);
+    }
+    int32_t next = -1;
+    if (hl) {
+      if (hr) stk[(sp++) * stride] = N.right;  // reference: push right, descend left
+      if (N.left < 0)
+        test_tri(S.tris, ~N.left, o, d, tmin, tr);
+      else
+        next = N.left;
+    } else if (hr) {
+      if (N.right < 0)
+        test_tri(S.tris, ~N.right, o, d, tmin, tr);
+      else
+        next = N.right;
+    }
+    while (next < 0) {  // pop: leaves are tested as they come off the stack
+      if (sp == 0) return tr;
+      int32_t x = stk[(--sp) * stride];
+      if (x < 0)
+        test_tri(S.tris, ~x, o, d, tmin, tr);
+      else
+        next = x;
+    }
+    node = next;
+  }
+}
+
+// --------------------------------------------------------------- generateRay
+__device__ inline void gen_ray(const mcpt_camera &cam, uint32_t idx, uint32_t idy, uint32_t w, uint32_t h,
+                               f4 &o, f4 &dir) {
+  // rayGenerator.cl:1-31 (NDRange {W, H}: width/height are size_t there)
+  size_t width = w, height = h;
+  float px = ((float)idx) / width, py = (float)idy / height;
+  float ratio = width * 1.0f / height;
+  const f4 cdir = (f4){cam.direction[0], cam.direction[1], cam.direction[2], cam.direction[3]};
+  const f4 chor = (f4){cam.horizontal[0], cam.horizontal[1], cam.horizontal[2], cam.horizontal[3]};
+  const f4 cup = (f4){cam.up[0], cam.up[1], cam.up[2], cam.up[3]};
+  const f4 ccen = (f4){cam.center[0], cam.center[1], cam.center[2], cam.center[3]};
+  if (cam.camera_type == 0) {
+    float temp1 = px - 0.5f;
+    float temp2 = py - 0.5f;
+    float distance = 0.5f / cl_tan(cam.arg / 2);
+    f4 dd = cdir * distance + temp1 * chor * ratio + temp2 * cup;
+    o = ccen;
+    dir = cl_normalize(dd);
+  } else {
+    o = ccen + (px - 0.5f) * (cam.arg) * (chor)*ratio + (py - 0.5f) * (cam.arg) * (cup);
+    dir = cl_normalize(cdir);
+  }
+  o.w = as_f(0);
+  dir.w = as_f((int32_t)(idy * w + idx));
+}
+
+// -------------------------------------------------------------------- shade
+struct ShadeIn {
+  f4 o, d;       // ray (o.w = term_depth bits, d.w = id bits)
+  f4 nrm;        // hit normal (flipped to face the ray)
+  f4 pt;         // hit point
+  int32_t mat;
+};
+struct ShadeOut {
+  f4 o, d;
+  f4 color;
+  bool new_ray;  // the reference writes rays[id] = newRay
+  bool bad;      // unknown material type (reference prints "Crash!!!")
+};
+
+// shade.cl:75-206 for one live ray that hit something.
+__device__ inline ShadeOut shade_hit(const mcpt_material *__restrict__ mats, const ShadeIn &in, f4 color,
+                                     uint32_t &seed, int max_depth) {
+  ShadeOut r;
+  r.bad = false;
+  r.new_ray = true;
+  const mcpt_material M = mats[in.mat];
+  const f4 kd = (f4){M.kd[0], M.kd[1], M.kd[2], M.kd[3]};
+  const f4 kaks = (f4){M.ka_ks[0], M.ka_ks[1], M.ka_ks[2], M.ka_ks[3]};
+  int32_t td = as_i(in.o.w);
+  f4 no, nd;
+  switch (M.type) {
+    case MCPT_DIFFUSE:
+    diffuse_lobe:
+      nd = random_dir(in.nrm, seed);
+      no = in.pt + kEps * nd;
+      no.w = as_f(td + 1);
+      nd.w = in.d.w;
+      color = color * kd * cl_dot3(nd.xyz, in.nrm.xyz) / (float)(2 * kClPi);
+      break;
+    case MCPT_GLOSSY:
+      if (lcg15(seed) & 0x00000001) {
+        f4 refl = mirror_dir(in.nrm, in.d);
+        nd = random_dir(refl, seed);
+        while (cl_dot3(nd.xyz, in.nrm.xyz) <= 0) nd = random_dir(refl, seed);
+        no = in.pt + kEps * nd;
+        no.w = as_f(td + 1);
+        nd.w = in.d.w;
+        color = color * kaks * cl_pow(cl_dot3(nd.xyz, refl.xyz), M.Ns) * cl_dot3(nd.xyz, in.nrm.xyz) /
+                (float)(2 * kClPi);
+      } else {
+        goto diffuse_lobe;
+      }
+      break;
+    case MCPT_LIGHT:
+      r.new_ray = false;
+      r.o = in.o;
+      r.o.w = as_f(td | (int32_t)MCPT_TERMINATED);
+      r.d = in.d;
+      r.color = color * kaks;
+      return r;
+    case MCPT_TRANSPARENT: {
+      bool inside = (td & 0x00FF0000) != 0;
+      float ei = inside ? M.Ni : 1.0f;
+      float et = inside ? 1.0f : M.Ni;
+      if (!transmit_dir(in.nrm, in.d, ei, et, nd)) {  // total internal reflection
+        no = in.pt;
+        nd = mirror_dir(in.nrm, in.d);
+        nd.w = in.d.w;
+        no.w = as_f(td + 1);
+        break;
+      }
+      float fr = fresnel(in.nrm, nd, M.Ni);
+      no = in.pt;
+      nd.w = in.d.w;
+      int32_t ntd = td + 1;
+      if ((lcg15(seed) * 1.0f / 32768) >= fr) {
+        ntd ^= 0x00FF0000;
+      } else {
+        nd.xyz = mirror_dir(in.nrm, in.d).xyz;
+      }
+      no.w = as_f(ntd);
+      break;
+    }
+    default:  // the reference leaves newRay uninitialised here; we end the path
+      r.bad = true;
+      r.new_ray = false;
+      r.o = in.o;
+      r.o.w = as_f(td | (int32_t)MCPT_TERMINATED);
+      r.d = in.d;
+      r.color = (f4){0.0f, 0.0f, 0.0f, 0.0f};
+      return r;
+  }
+  int32_t ntd = as_i(no.w);
+  if ((ntd & 0x0000FFFF) >= max_depth) {
+    color = (f4){0.0f, 0.0f, 0.0f, 0.0f};
+    no.w = as_f(ntd | (int32_t)MCPT_TERMINATED);
+  }
+  r.o = no;
+  r.d = nd;
+  r.color = color;
+  return r;
+}
+
+// history.cl:3-28 on one pixel; returns the colour the reference shows.
+__device__ inline f4 accumulate_one(f4 now, f4 &hist, int32_t &cnt, int max_attempt) {
+  if (cl_length4(now) == 0 || cnt >= max_attempt) return hist;
+  now = (now + hist * cnt) / (cnt + 1);
+  hist = now;
+  hist.w = 0.0f;
+  ++cnt;
+  return now;
+}
+
+// --------------------------------------------------------- fused hot kernel
+struct RenderArgs {
+  mcpt_camera cam;
+  SceneView S;
+  uint32_t *seeds;
+  f4 *hist;
+  int32_t *count;
+  unsigned long long *stats;
+  int32_t W, H, local_rows, tiles_x;
+  int32_t stripe_rows, stripe_index, stripe_count;
+  int32_t max_depth, max_attempt, frame_begin, frames;
+  int32_t stack_depth;
+};
+
+__device__ inline int32_t global_row(int32_t lr, const RenderArgs &A) {
+  int32_t s = lr / A.stripe_rows;
+  return (s * A.stripe_count + A.stripe_index) * A.stripe_rows + lr % A.stripe_rows;
+}
+
+constexpr float kTmin = 0.001f;  // host EPSILON passed as tmin (oclbasic.h:193, scenebuild.cpp:125)
+
+template <int MODE, bool STATS>
+__global__ void __launch_bounds__(64) k_render(RenderArgs A) {
+  extern __shared__ int32_t lds_stack[];
+  const int lane = threadIdx.x;
+  int32_t *stk = lds_stack + lane;  // column-major [depth][64]: conflict-free
+  const int32_t tile = blockIdx.x;
+  const int32_t x = (tile % A.tiles_x) * 8 + (lane & 7);
+  const int32_t lr = (tile / A.tiles_x) * 8 + (lane >> 3);
+  if (x >= A.W || lr >= A.local_rows) return;
+  const int32_t y = global_row(lr, A);
+  if (y >= A.H) return;
+  const int32_t pid = y * A.W + x;
+
+  uint32_t seed = A.seeds[pid];
+  f4 hist = A.hist[pid];
+  int32_t cnt = A.count[pid];
+  f4 o0, d0;
+  gen_ray(A.cam, (uint32_t)x, (uint32_t)y, (uint32_t)A.W, (uint32_t)A.H, o0, d0);
+
+  unsigned long long n_seg = 0, n_nodes = 0, n_tests = 0, n_bad = 0;
+  int32_t f = 0;
+  f4 o = o0, d = d0;
+  f4 color = (f4){1.0f, 1.0f, 1.0f, 1.0f};
+  while (f < A.frames) {
+    // intersect.cl: trace one segment
+    Trace tr = MODE == MCPT_MODE_NOPRUNE ? traverse<false, true>(A.S, o.xyz, d.xyz, kTmin, stk, 64)
+                                         : traverse<true, false>(A.S, o.xyz, d.xyz, kTmin, stk, 64);
+    if (STATS) {
+      n_seg++;
+      n_nodes += tr.nodes;
+      n_tests += tr.tests;
+    }
+    bool done;
+    if (tr.t >= kFltMax) {  // shade.cl:92-96 — miss: black, terminate
+      color = (f4){0.0f, 0.0f, 0.0f, 0.0f};
+      done = true;
+    } else {
+      const DevTri &T = A.S.tris[tr.tri];
+      ShadeIn in;
+      in.o = o;
+      in.d = d;
+      in.nrm = (f4){T.nrm.x, T.nrm.y, T.nrm.z, 0.0f};
+      if (cl_dot3(d.xyz, in.nrm.xyz) > 0) in.nrm = -in.nrm;  // intersect.cl:23-25
+      in.pt = o + tr.t * d;                                    // objdef.h:218
+      in.mat = as_i(T.nrm.w);
+      ShadeOut so = shade_hit(A.S.mats, in, color, seed, A.max_depth);
+      if (STATS) n_bad += so.bad;
+      color = so.color;
+      o = so.o;
+      d = so.d;
+      done = (as_i(o.w) & (int32_t)MCPT_TERMINATED) != 0;
+    }
+    if (done) {
+      // ColorOut: history runs while attemptCount <= MAX_ATTEMPT (colorout.cpp:56)
+      if (A.frame_begin + f <= A.max_attempt) (void)accumulate_one(color, hist, cnt, A.max_attempt);
+      ++f;
+      o = o0;  // no jitter: every frame re-shoots the same primary ray
+      d = d0;
+      color = (f4){1.0f, 1.0f, 1.0f, 1.0f};
+    }
+  }
+  A.seeds[pid] = seed;
+  A.hist[pid] = hist;
+  A.count[pid] = cnt;
+  if (STATS) {
+    atomicAdd(&A.stats[0], n_seg);
+    atomicAdd(&A.stats[1], n_nodes);
+    atomicAdd(&A.stats[2], n_tests);
+    if (n_bad) atomicAdd(&A.stats[3], n_bad);
+  }
+}
+
+// ------------------------------------------------------ wavefront kernels
+__global__ void k_generate(mcpt_camera cam, uint32_t w, uint32_t h, mcpt_ray *rays) {
+  uint32_t x = blockIdx.x * blockDim.x + threadIdx.x, y = blockIdx.y;
+  if (x >= w || y >= h) return;
+  f4 o, d;
+  gen_ray(cam, x, y, w, h, o, d);
+  mcpt_ray &r = rays[(size_t)y * w + x];
+  *(f4 *)r.origin = o;
+  *(f4 *)r.direction = d;
+}
+
+template <int MODE>
+__global__ void __launch_bounds__(64) k_intersect(SceneView S, const mcpt_ray *rays, int64_t n, mcpt_hit *hits,
+                                                  float tmin) {
+  extern __shared__ int32_t lds_stack[];
+  int64_t id = (int64_t)blockIdx.x * 64 + threadIdx.x;
+  if (id >= n) return;
+  const f4 o = *(const f4 *)rays[id].origin;
+  const f4 d = *(const f4 *)rays[id].direction;
+  if (as_i(o.w) & (int32_t)0xFF000000) return;  // intersect.cl:16-18 (hit left untouched)
+  Trace tr = MODE == MCPT_MODE_NOPRUNE ? traverse<false, true>(S, o.xyz, d.xyz, tmin, lds_stack + threadIdx.x, 64)
+                                       : traverse<true, false>(S, o.xyz, d.xyz, tmin, lds_stack + threadIdx.x, 64);
+  mcpt_hit h;
+  f4 nrm = (f4){0.0f, 0.0f, 0.0f, 0.0f}, pt = (f4){0.0f, 0.0f, 0.0f, 0.0f};
+  h.t = tr.t;
+  h.triangle_id = 0;
+  h.material_id = 0;
+  h.pad = 0;
+  if (tr.tri >= 0) {
+    const DevTri &T = S.tris[tr.tri];
+    nrm = (f4){T.nrm.x, T.nrm.y, T.nrm.z, 0.0f};
+    pt = o + tr.t * d;
+    h.material_id = (uint32_t)as_i(T.nrm.w);
+  }
+  if (tr.last >= 0) {
+    h.triangle_id = (uint32_t)(MODE == MCPT_MODE_NOPRUNE ? tr.last : tr.tri);
+    if (cl_dot3(d.xyz, nrm.xyz) > 0) nrm = -nrm;
+  }
+  *(f4 *)h.normal = nrm;
+  *(f4 *)h.point = pt;
+  hits[id] = h;
+}
+
+__global__ void k_shade(const mcpt_material *mats, mcpt_ray *rays, const mcpt_hit *hits, f4 *colors,
+                        uint32_t *seeds, int64_t n, int max_depth) {
+  int64_t id = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (id >= n) return;
+  mcpt_ray &R = rays[id];
+  const mcpt_hit &H = hits[id];
+  f4 o = *(f4 *)R.origin;
+  if (as_i(o.w) & (int32_t)0xFF000000) return;  // shade.cl:86-88
+  if (H.t >= kFltMax) {                          // shade.cl:89-93
+    colors[id] = (f4){0.0f, 0.0f, 0.0f, 0.0f};
+    R.origin[3] = as_f(as_i(o.w) | (int32_t)0xFF000000);
+    return;
+  }
+  ShadeIn in;
+  in.o = o;
+  in.d = *(f4 *)R.direction;
+  in.nrm = *(const f4 *)H.normal;
+  in.pt = *(const f4 *)H.point;
+  in.mat = (int32_t)H.material_id;
+  uint32_t seed = seeds[id];
+  ShadeOut so = shade_hit(mats, in, colors[id], seed, max_depth);
+  colors[id] = so.color;
+  seeds[id] = seed;
+  if (so.new_ray) {
+    *(f4 *)R.origin = so.o;
+    *(f4 *)R.direction = so.d;
+    *(f4 *)R.ratio = (f4){0.0f, 0.0f, 0.0f, 0.0f};
+  } else {
+    R.origin[3] = so.o.w;
+  }
+}
+
+__global__ void k_accumulate(f4 *colors, f4 *hist, int32_t *count, int64_t n, int max_attempt) {
+  int64_t id = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (id >= n) return;
+  f4 h = hist[id];
+  int32_t c = count[id];
+  colors[id] = accumulate_one(colors[id], h, c, max_attempt);
+  hist[id] = h;
+  count[id] = c;
+}
+
+// =================================================================== ABI
+extern "C" {
+
+const char *mcpt_version(void) { return "mcpt-mi355x 0.1 (gfx950)"; }
+
+int mcpt_device_count(int32_t *count) {
+  if (!count) return mcpt::fail(MCPT_ERR_ARG, "device_count: null");
+  int n = 0;
+  hipError_t e = hipGetDeviceCount(&n);
+  *count = e == hipSuccess ? n : 0;
+  return MCPT_OK;
+}
+
+int mcpt_ctx_create(int32_t device, mcpt_ctx **out) {
+  if (!out) return mcpt::fail(MCPT_ERR_ARG, "ctx_create: null out");
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess || n == 0) return mcpt::fail(MCPT_ERR_NOGPU, "ctx_create: no HIP device");
+  if (device < 0 || device >= n) return mcpt::fail(MCPT_ERR_NOGPU, "ctx_create: device index out of range");
+  HIP_OK(hipSetDevice(device));
+  mcpt_ctx *c = new mcpt_ctx();
+  c->device = device;
+  std::memset(&c->last, 0, sizeof(c->last));
+  if (hipMalloc(&c->d_stats, 4 * sizeof(unsigned long long)) != hipSuccess ||
+      hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess) {
+    delete c;
+    return mcpt::fail(MCPT_ERR_HIP, "ctx_create: allocation failed");
+  }
+  *out = c;
+  return MCPT_OK;
+}
+
+int mcpt_ctx_destroy(mcpt_ctx *c) {
+  if (!c) return MCPT_OK;
+  (void)hipSetDevice(c->device);
+  if (c->d_stats) (void)hipFree(c->d_stats);
+  if (c->ev0) (void)hipEventDestroy(c->ev0);
+  if (c->ev1) (void)hipEventDestroy(c->ev1);
+  delete c;
+  return MCPT_OK;
+}
+
+int mcpt_set_stats(mcpt_ctx *c, int32_t on) {
+  if (!c) return mcpt::fail(MCPT_ERR_ARG, "set_stats: null ctx");
+  c->stats_on = on != 0;
+  return MCPT_OK;
+}
+
+int mcpt_get_stats(mcpt_ctx *c, mcpt_stats *out) {
+  if (!c || !out) return mcpt::fail(MCPT_ERR_ARG, "get_stats: null");
+  *out = c->last;
+  return MCPT_OK;
+}
+
+int mcpt_scene_upload(mcpt_ctx *ctx, const mcpt_triangle *tris, int64_t n_tris, const mcpt_bvh_node *nodes,
+                      int64_t n_nodes, const mcpt_material *mats, int32_t n_mats, mcpt_scene **out) {
+  if (!ctx || !tris || !nodes || !mats || !out || n_tris <= 0 || n_mats <= 0)
+    return mcpt::fail(MCPT_ERR_ARG, "scene_upload: bad argument");
+  if (n_nodes != 2 * n_tris - 1) return mcpt::fail(MCPT_ERR_ARG, "scene_upload: expected 2n-1 BVH nodes");
+  int32_t depth = 0;
+  int rc = mcpt_bvh_stack_depth(nodes, n_nodes, &depth);
+  if (rc) return rc;
+  if (depth > 64) return mcpt::fail(MCPT_ERR_LIMIT, "scene_upload: BVH deeper than the reference's 64-entry stack");
+  const int64_t n = n_tris;
+  // validate links and material ids before anything reaches the GPU
+  for (int64_t i = 0; i < n_nodes; ++i) {
+    const mcpt_bvh_node &b = nodes[i];
+    if (b.left < 0 || b.right < 0) return mcpt::fail(MCPT_ERR_ARG, "scene_upload: negative child index");
+    if (b.left == b.right) {
+      if (b.left >= n) return mcpt::fail(MCPT_ERR_ARG, "scene_upload: leaf triangle index out of range");
+    } else if (b.left >= n_nodes || b.right >= n_nodes) {
+      return mcpt::fail(MCPT_ERR_ARG, "scene_upload: child index out of range");
+    }
+  }
+  for (int64_t i = 0; i < n; ++i) {
+    int32_t m;
+    std::memcpy(&m, &tris[i].normal[3], 4);
+    if (m < 0 || m >= n_mats) return mcpt::fail(MCPT_ERR_ARG, "scene_upload: triangle material id out of range");
+  }
+  // reference node index -> device index: internal nodes keep their index in
+  // a compacted array (the HLBVH puts them at [0, n-2]); leaves become ~tri.
+  std::vector<int32_t> remap(n_nodes, -1);
+  int64_t n_int = 0;
+  for (int64_t i = 0; i < n_nodes; ++i)
+    if (nodes[i].left != nodes[i].right) remap[i] = (int32_t)n_int++;
+  auto child = [&](int32_t c) -> int32_t { return nodes[c].left == nodes[c].right ? ~nodes[c].left : remap[c]; };
+  std::vector<DevNode> dn(std::max<int64_t>(n_int, 1));
+  std::memset(dn.data(), 0, dn.size() * sizeof(DevNode));
+  for (int64_t i = 0; i < n_nodes; ++i) {
+    if (remap[i] < 0) continue;
+    const mcpt_bvh_node &b = nodes[i], &L = nodes[b.left], &R = nodes[b.right];
+    DevNode &d = dn[remap[i]];
+    d.a = (f4){L.bbmin[0], L.bbmin[1], L.bbmin[2], L.bbmax[0]};
+    d.b = (f4){L.bbmax[1], L.bbmax[2], R.bbmin[0], R.bbmin[1]};
+    d.c = (f4){R.bbmin[2], R.bbmax[0], R.bbmax[1], R.bbmax[2]};
+    d.left = child(b.left);
+    d.right = child(b.right);
+  }
+  if (n_int > 0 && remap[0] != 0) return mcpt::fail(MCPT_ERR_ARG, "scene_upload: root must be node 0");
+  std::vector<DevTri> dt(n);
+  for (int64_t i = 0; i < n; ++i) {
+    const mcpt_triangle &t = tris[i];
+    DevTri &d = dt[i];
+    // objdef.h:190-199: AB = (v1 - v0).s012, AC = (v2 - v0).s012, matrix rows -AB, -AC
+    d.v0 = (f4){t.v[0][0], t.v[0][1], t.v[0][2], 0.0f};
+    d.nab = (f4){-(t.v[1][0] - t.v[0][0]), -(t.v[1][1] - t.v[0][1]), -(t.v[1][2] - t.v[0][2]), 0.0f};
+    d.nac = (f4){-(t.v[2][0] - t.v[0][0]), -(t.v[2][1] - t.v[0][1]), -(t.v[2][2] - t.v[0][2]), 0.0f};
+    d.nrm = (f4){t.normal[0], t.normal[1], t.normal[2], t.normal[3]};
+  }
+  // pruning margin: 2^-10 of the scene diagonal
+  const mcpt_bvh_node &root = nodes[0];
+  float dx = root.bbmax[0] - root.bbmin[0], dy = root.bbmax[1] - root.bbmin[1], dz = root.bbmax[2] - root.bbmin[2];
+  float diag = std::sqrt(dx * dx + dy * dy + dz * dz);
+
+  HIP_OK(hipSetDevice(ctx->device));
+  mcpt_scene *s = new mcpt_scene();
+  s->device = ctx->device;
+  if (hipMalloc(&s->nodes, dn.size() * sizeof(DevNode)) != hipSuccess ||
+      hipMalloc(&s->tris, dt.size() * sizeof(DevTri)) != hipSuccess ||
+      hipMalloc(&s->mats, n_mats * sizeof(mcpt_material)) != hipSuccess) {
+    mcpt_scene_destroy(s);
+    return mcpt::fail(MCPT_ERR_HIP, "scene_upload: hipMalloc failed");
+  }
+  if (hipMemcpy(s->nodes, dn.data(), dn.size() * sizeof(DevNode), hipMemcpyHostToDevice) != hipSuccess ||
+      hipMemcpy(s->tris, dt.data(), dt.size() * sizeof(DevTri), hipMemcpyHostToDevice) != hipSuccess ||
+      hipMemcpy(s->mats, mats, n_mats * sizeof(mcpt_material), hipMemcpyHostToDevice) != hipSuccess) {
+    mcpt_scene_destroy(s);
+    return mcpt::fail(MCPT_ERR_HIP, "scene_upload: hipMemcpy failed");
+  }
+  s->n_tris = n;
+  s->n_internal = n_int;
+  s->n_mats = n_mats;
+  s->stack_depth = std::max(depth, 1);
+  SceneView &v = s->view;
+  v.nodes = s->nodes;
+  v.tris = s->tris;
+  v.mats = s->mats;
+  v.root_min = (f4){root.bbmin[0], root.bbmin[1], root.bbmin[2], root.bbmin[3]};
+  v.root_max = (f4){root.bbmax[0], root.bbmax[1], root.bbmax[2], root.bbmax[3]};
+  v.root_leaf = root.left == root.right ? root.left : -1;
+  v.n_mats = n_mats;
+  v.prune_margin = std::isfinite(diag) ? std::ldexp(diag, -10) : __builtin_inff();
+  *out = s;
+  return MCPT_OK;
+}
+
+int mcpt_scene_destroy(mcpt_scene *s) {
+  if (!s) return MCPT_OK;
+  (void)hipSetDevice(s->device);
+  if (s->nodes) (void)hipFree(s->nodes);
+  if (s->tris) (void)hipFree(s->tris);
+  if (s->mats) (void)hipFree(s->mats);
+  delete s;
+  return MCPT_OK;
+}
+
+static int check_render(const mcpt_render_params *p) {
+  if (p->width <= 0 || p->height <= 0 || p->max_depth <= 0 || p->max_depth > 0xFFFF || p->frames < 0 ||
+      p->frame_begin < 0 || p->stripe_count <= 0 || p->stripe_rows <= 0 || p->stripe_index < 0 ||
+      p->stripe_index >= p->stripe_count || (int64_t)p->width * p->height > (int64_t)INT32_MAX)
+    return mcpt::fail(MCPT_ERR_ARG, "render: bad parameters");
+  if (p->mode != MCPT_MODE_EXACT && p->mode != MCPT_MODE_NOPRUNE) return mcpt::fail(MCPT_ERR_ARG, "render: bad mode");
+  return MCPT_OK;
+}
+
+int mcpt_render_frames(mcpt_ctx *ctx, const mcpt_scene *scene, const mcpt_camera *cam, const mcpt_render_params *p,
+                       uint32_t *seeds, float *hist, int32_t *count, void *stream) {
+  if (!ctx || !scene || !cam || !p || !seeds || !hist || !count) return mcpt::fail(MCPT_ERR_ARG, "render: null argument");
+  int rc = check_render(p);
+  if (rc) return rc;
+  HIP_OK(hipSetDevice(ctx->device));
+  hipStream_t st = (hipStream_t)stream;
+  RenderArgs A;
+  A.cam = *cam;
+  A.S = scene->view;
+  A.seeds = seeds;
+  A.hist = (f4 *)hist;
+  A.count = count;
+  A.stats = ctx->d_stats;
+  A.W = p->width;
+  A.H = p->height;
+  A.stripe_rows = p->stripe_rows;
+  A.stripe_index = p->stripe_index;
+  A.stripe_count = p->stripe_count;
+  // rows owned by this stripe residue
+  int32_t full = p->height / (p->stripe_rows * p->stripe_count);
+  int32_t rem = p->height - full * p->stripe_rows * p->stripe_count;
+  int32_t extra = std::min(std::max(rem - p->stripe_index * p->stripe_rows, 0), p->stripe_rows);
+  A.local_rows = full * p->stripe_rows + extra;
+  A.tiles_x = (p->width + 7) / 8;
+  A.max_depth = p->max_depth;
+  A.max_attempt = p->max_attempt;
+  A.stack_depth = scene->stack_depth;
+  const int64_t tiles = (int64_t)A.tiles_x * ((A.local_rows + 7) / 8);
+  const size_t lds = (size_t)scene->stack_depth * 64 * sizeof(int32_t);
+  int fpl = p->frames_per_launch;
+  if (fpl <= 0) {  // aim for ~2^26 lane-frames per launch: long enough to amortise, short enough to stream
+    int64_t px = (int64_t)p->width * A.local_rows;
+    fpl = (int)std::max<int64_t>(1, std::min<int64_t>(p->frames, (int64_t(1) << 26) / std::max<int64_t>(px, 1)));
+  }
+  if (ctx->stats_on) HIP_OK(hipMemsetAsync(ctx->d_stats, 0, 4 * sizeof(unsigned long long), st));
+  HIP_OK(hipEventRecord(ctx->ev0, st));
+  int launches = 0;
+  if (tiles > 0 && p->frames > 0) {
+    for (int f0 = 0; f0 < p->frames; f0 += fpl) {
+      A.frame_begin = p->frame_begin + f0;
+      A.frames = std::min(fpl, p->frames - f0);
+      if (p->mode == MCPT_MODE_NOPRUNE) {
+        if (ctx->stats_on)
+          hipLaunchKernelGGL((k_render<MCPT_MODE_NOPRUNE, true>), dim3(tiles), dim3(64), lds, st, A);
+        else
+          hipLaunchKernelGGL((k_render<MCPT_MODE_NOPRUNE, false>), dim3(tiles), dim3(64), lds, st, A);
+      } else {
+        if (ctx->stats_on)
+          hipLaunchKernelGGL((k_render<MCPT_MODE_EXACT, true>), dim3(tiles), dim3(64), lds, st, A);
+        else
+          hipLaunchKernelGGL((k_render<MCPT_MODE_EXACT, false>), dim3(tiles), dim3(64), lds, st, A);
+      }
+      HIP_OK(hipGetLastError());
+      ++launches;
+    }
+  }
+  HIP_OK(hipEventRecord(ctx->ev1, st));
+  HIP_OK(hipEventSynchronize(ctx->ev1));
+  float ms = 0.0f;
+  HIP_OK(hipEventElapsedTime(&ms, ctx->ev0, ctx->ev1));
+  std::memset(&ctx->last, 0, sizeof(ctx->last));
+  ctx->last.kernel_ms = ms;
+  ctx->last.launches = launches;
+  if (ctx->stats_on) {
+    unsigned long long h[4];
+    HIP_OK(hipMemcpy(h, ctx->d_stats, sizeof(h), hipMemcpyDeviceToHost));
+    ctx->last.segments = h[0];
+    ctx->last.node_visits = h[1];
+    ctx->last.tri_tests = h[2];
+    ctx->last.bad_material = h[3];
+  }
+  return MCPT_OK;
+}
+
+int mcpt_generate_rays(mcpt_ctx *ctx, const mcpt_camera *cam, int32_t w, int32_t h, mcpt_ray *rays, void *stream) {
+  if (!ctx || !cam || !rays || w <= 0 || h <= 0) return mcpt::fail(MCPT_ERR_ARG, "generate_rays: bad argument");
+  HIP_OK(hipSetDevice(ctx->device));
+  hipLaunchKernelGGL(k_generate, dim3((w + 63) / 64, h), dim3(64), 0, (hipStream_t)stream, *cam, (uint32_t)w,
+                     (uint32_t)h, rays);
+  HIP_OK(hipGetLastError());
+  return MCPT_OK;
+}
+
+int mcpt_intersect(mcpt_ctx *ctx, const mcpt_scene *scene, const mcpt_ray *rays, int64_t n, mcpt_hit *hits,
+                   float tmin, int32_t mode, void *stream) {
+  if (!ctx || !scene || !rays || !hits || n < 0) return mcpt::fail(MCPT_ERR_ARG, "intersect: bad argument");
+  if (n == 0) return MCPT_OK;
+  HIP_OK(hipSetDevice(ctx->device));
+  size_t lds = (size_t)scene->stack_depth * 64 * sizeof(int32_t);
+  dim3 g((unsigned)((n + 63) / 64));
+  if (mode == MCPT_MODE_NOPRUNE)
+    hipLaunchKernelGGL(k_intersect<MCPT_MODE_NOPRUNE>, g, dim3(64), lds, (hipStream_t)stream, scene->view, rays, n,
+                       hits, tmin);
+  else
+    hipLaunchKernelGGL(k_intersect<MCPT_MODE_EXACT>, g, dim3(64), lds, (hipStream_t)stream, scene->view, rays, n,
+                       hits, tmin);
+  HIP_OK(hipGetLastError());
+  return MCPT_OK;
+}
+
+int mcpt_shade(mcpt_ctx *ctx, const mcpt_scene *scene, mcpt_ray *rays, const mcpt_hit *hits, float *color,
+               uint32_t *seeds, int64_t n, int32_t max_depth, void *stream) {
+  if (!ctx || !scene || !rays || !hits || !color || !seeds || n < 0 || max_depth <= 0)
+    return mcpt::fail(MCPT_ERR_ARG, "shade: bad argument");
+  if (n == 0) return MCPT_OK;
+  HIP_OK(hipSetDevice(ctx->device));
+  hipLaunchKernelGGL(k_shade, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream, scene->mats, rays,
+                     hits, (f4 *)color, seeds, n, max_depth);
+  HIP_OK(hipGetLastError());
+  return MCPT_OK;
+}
+
+int mcpt_accumulate(mcpt_ctx *ctx, float *color, float *hist, int32_t *count, int64_t n, int32_t max_attempt,
+                    void *stream) {
+  if (!ctx || !color || !hist || !count || n < 0) return mcpt::fail(MCPT_ERR_ARG, "accumulate: bad argument");
+  if (n == 0) return MCPT_OK;
+  HIP_OK(hipSetDevice(ctx->device));
+  hipLaunchKernelGGL(k_accumulate, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream, (f4 *)color,
+                     (f4 *)hist, count, n, max_attempt);
+  HIP_OK(hipGetLastError());
+  return MCPT_OK;
+}
+
+}  // extern "C"

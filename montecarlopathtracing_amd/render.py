@@ -1,0 +1,181 @@
+"""Device-side driver over libmcpt_hip.so: the reference's OpenCL::init/update
+frame loop (MCPT/OpenCLApp.cpp:36-82), RayGeneration (raygeneration.cpp),
+SceneBuild/SceneCL (scenebuild.cpp) and ColorOut (colorout.cpp) on one GPU.
+
+PyTorch only provides device memory and the stream; every kernel is the HIP
+code in csrc/mcpt_device.hip.  Buffers are raw byte tensors holding the
+reference's record layouts.
+"""
+import ctypes
+
+import numpy as np
+import torch
+
+from . import _lib as L
+
+
+def _stream():
+    return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
+def _dev_bytes(nbytes, device):
+    return torch.empty(max(int(nbytes), 1), dtype=torch.uint8, device=device)
+
+
+def default_seeds(n, variant="splitmix"):
+    """Per-pixel 32-bit seeds.  The reference draws them with srand(time); rand()
+    (scenebuild.cpp:113-120) — non-deterministic — so parity runs take seeds as
+    an input.  'splitmix': splitmix64(0x5EED ^ i) & 0xFFFFFFFF;
+    'msvc15' keeps 15 bits like MSVC's rand()."""
+    i = np.arange(n, dtype=np.uint64)
+    with np.errstate(over="ignore"):
+        z = (np.uint64(0x5EED) ^ i) + np.uint64(0x9E3779B97F4A7C15)
+        z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+        z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+        z = z ^ (z >> np.uint64(31))
+    s = (z & np.uint64(0xFFFFFFFF)).astype(np.uint32)
+    if variant == "msvc15":
+        s &= np.uint32(0x7FFF)
+    return s
+
+
+class DeviceScene:
+    """SceneBuild::buildScene result living in HBM (child-box node layout)."""
+
+    def __init__(self, renderer, data):
+        self.renderer = renderer
+        self.data = data
+        self.handle = ctypes.c_void_p()
+        t = np.ascontiguousarray(data.tris)
+        nd = np.ascontiguousarray(data.nodes)
+        m = np.ascontiguousarray(data.mats)
+        L.check(L.lib().mcpt_scene_upload(renderer.ctx, L.ptr(t), len(t), L.ptr(nd), len(nd), L.ptr(m), len(m),
+                                          ctypes.byref(self.handle)))
+
+    def close(self):
+        if self.handle:
+            L.lib().mcpt_scene_destroy(self.handle)
+            self.handle = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class ImageState:
+    """Per-pixel state that persists across frames: seed chain (randBuffer),
+    accumulated mean (frameBuffer) and sample count (sampleCount)."""
+
+    def __init__(self, width, height, seeds, device):
+        n = width * height
+        self.width, self.height = width, height
+        self.seeds = torch.from_numpy(np.ascontiguousarray(seeds, np.uint32).view(np.int32)).to(device)
+        self.hist = torch.zeros((n, 4), dtype=torch.float32, device=device)
+        self.count = torch.zeros(n, dtype=torch.int32, device=device)
+        self.frames_done = 0
+
+    def image(self):
+        """(H, W, 4) float32 accumulated image, row 0 = bottom (GL convention)."""
+        return self.hist.cpu().numpy().reshape(self.height, self.width, 4)
+
+    def seeds_np(self):
+        return self.seeds.cpu().numpy().view(np.uint32)
+
+
+class Renderer:
+    """One GPU context (OpenCLBasic::init equivalent)."""
+
+    def __init__(self, device=0):
+        if not torch.cuda.is_available():
+            raise L.MCPTError("no GPU: the HIP path has no CPU fallback")
+        self.device = torch.device("cuda", device)
+        torch.cuda.set_device(self.device)
+        self.ctx = ctypes.c_void_p()
+        L.check(L.lib().mcpt_ctx_create(device, ctypes.byref(self.ctx)))
+
+    def close(self):
+        if self.ctx:
+            L.lib().mcpt_ctx_destroy(self.ctx)
+            self.ctx = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def upload(self, data):
+        return DeviceScene(self, data)
+
+    def set_stats(self, on):
+        L.check(L.lib().mcpt_set_stats(self.ctx, int(bool(on))))
+
+    def stats(self):
+        s = L.Stats()
+        L.check(L.lib().mcpt_get_stats(self.ctx, ctypes.byref(s)))
+        return {f: getattr(s, f) for f, _ in L.Stats._fields_ if f != "pad"}
+
+    def new_state(self, width, height, seeds=None):
+        if seeds is None:
+            seeds = default_seeds(width * height)
+        return ImageState(width, height, seeds, self.device)
+
+    # ---------------------------------------------------------- fused path
+    def render_frames(self, scene, camera, state, max_depth, max_attempt, frames, frame_begin=None,
+                      stripe_rows=16, stripe_index=0, stripe_count=1, mode=L.MODE_EXACT,
+                      frames_per_launch=0):
+        """Frames [frame_begin, frame_begin+frames) for this GPU's row stripes
+        (OpenCL::update x frames + ColorOut accumulation)."""
+        p = L.RenderParams()
+        p.width, p.height = state.width, state.height
+        p.max_depth, p.max_attempt = int(max_depth), int(max_attempt)
+        p.frame_begin = state.frames_done if frame_begin is None else int(frame_begin)
+        p.frames = int(frames)
+        p.stripe_rows, p.stripe_index, p.stripe_count = int(stripe_rows), int(stripe_index), int(stripe_count)
+        p.mode = int(mode)
+        p.frames_per_launch = int(frames_per_launch)
+        cam = np.ascontiguousarray(camera)
+        L.check(L.lib().mcpt_render_frames(self.ctx, scene.handle, L.ptr(cam), ctypes.byref(p), L.ptr(state.seeds),
+                                           L.ptr(state.hist), L.ptr(state.count), _stream()))
+        state.frames_done = p.frame_begin + p.frames
+        return state
+
+    # ------------------------------------------------ wavefront (drop-in)
+    def generate_rays(self, camera, width, height):
+        """rayGenerator.cl: W*H Ray records (device bytes)."""
+        rays = _dev_bytes(width * height * L.RAY.itemsize, self.device)
+        cam = np.ascontiguousarray(camera)
+        L.check(L.lib().mcpt_generate_rays(self.ctx, L.ptr(cam), width, height, L.ptr(rays), _stream()))
+        return rays
+
+    def intersect(self, scene, rays, hits=None, tmin=0.001, mode=L.MODE_EXACT):
+        """intersect.cl on a ray buffer; returns the Hit buffer."""
+        n = rays.numel() // L.RAY.itemsize
+        if hits is None:
+            hits = torch.zeros(n * L.HIT.itemsize, dtype=torch.uint8, device=self.device)
+        L.check(L.lib().mcpt_intersect(self.ctx, scene.handle, L.ptr(rays), n, L.ptr(hits), float(tmin), int(mode),
+                                       _stream()))
+        return hits
+
+    def shade(self, scene, rays, hits, color, seeds, max_depth):
+        """shade.cl on (rays, hits, colour, seeds) in place."""
+        n = rays.numel() // L.RAY.itemsize
+        L.check(L.lib().mcpt_shade(self.ctx, scene.handle, L.ptr(rays), L.ptr(hits), L.ptr(color), L.ptr(seeds), n,
+                                   int(max_depth), _stream()))
+
+    def accumulate(self, color, hist, count, max_attempt):
+        """history.cl: running mean of non-zero samples."""
+        n = count.numel()
+        L.check(L.lib().mcpt_accumulate(self.ctx, L.ptr(color), L.ptr(hist), L.ptr(count), n, int(max_attempt),
+                                        _stream()))
+
+
+def records(buf, dtype):
+    """View a device byte buffer as host numpy records."""
+    return buf.cpu().numpy().view(dtype)
+
+
+def to_device(arr, device):
+    return torch.from_numpy(np.ascontiguousarray(arr).view(np.uint8).reshape(-1)).to(device)

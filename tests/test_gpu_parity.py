@@ -1,0 +1,189 @@
+"""GPU parity: the HIP path (libmcpt_hip.so) against the reference's own OpenCL
+kernels compiled for gfx950 (oracle/_ref, tests/refgpu.py) on the same inputs.
+
+Bar: bit-exact.  Rays, hits, shade transitions, accumulated images, counts
+and seed chains must match the reference kernels bit for bit.
+Only Hit.triangle_id is exempt in the pruned mode: it is the reference's
+"last accepted triangle" (objdef.h:262-265), which shade never reads; the
+NOPRUNE mode reproduces it too.
+"""
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+
+pytestmark = pytest.mark.gpu
+
+from montecarlopathtracing_amd import _lib as L  # noqa: E402
+from montecarlopathtracing_amd import render as R  # noqa: E402
+from montecarlopathtracing_amd import scene as S  # noqa: E402
+
+from . import refgpu, scenes  # noqa: E402
+
+needs_ref = pytest.mark.skipif(not refgpu.available(), reason="oracle/_ref not built (needs /root/reference at build time)")
+
+
+@pytest.fixture(scope="module")
+def rnd():
+    return R.Renderer(0)
+
+
+def bits(a):
+    return np.ascontiguousarray(a).view(np.uint8)
+
+
+def assert_bits_equal(a, b, what):
+    a, b = np.ascontiguousarray(a), np.ascontiguousarray(b)
+    same = bits(a) == bits(b)
+    if not same.all():
+        ia = np.nonzero(~same.reshape(len(a), -1).all(axis=1))[0]
+        raise AssertionError("%s: %d / %d records differ, first %s\nmine=%r\nref =%r" % (
+            what, len(ia), len(a), ia[:8], a[ia[:2]], b[ia[:2]]))
+
+
+def ray_fields_equal(mine, ref, what):
+    assert_bits_equal(mine["origin"], ref["origin"], what + ".origin")
+    assert_bits_equal(mine["direction"], ref["direction"], what + ".direction")
+
+
+def hit_fields_equal(mine, ref, live, what, check_tri=False):
+    m, r = mine[live], ref[live]
+    for f in ("t", "normal", "point", "material_id"):
+        assert_bits_equal(m[f], r[f], what + "." + f)
+    if check_tri:
+        assert_bits_equal(m["triangle_id"], r["triangle_id"], what + ".triangle_id")
+
+
+SCENES = [("cbox", scenes.cbox, scenes.CBOX_CAM), ("mis", scenes.mis, scenes.MIS_CAM)]
+
+
+@needs_ref
+@pytest.mark.parametrize("w,h", [(64, 48), (37, 21)])
+@pytest.mark.parametrize("camjson", [scenes.CBOX_CAM, scenes.MIS_CAM, scenes.DINING_CAM])
+def test_generate_rays_bitexact(rnd, camjson, w, h):
+    cam = S.parse_camera(camjson)
+    mine = R.records(rnd.generate_rays(cam, w, h), L.RAY)
+    ref = refgpu.generate(cam, w, h)
+    ray_fields_equal(mine, ref, "generateRay")
+
+
+def _bounce_chain(rnd, data, camjson, w, h, depth, mode):
+    """Run intersect+shade bounce by bounce on BOTH implementations, feeding
+    each stage the reference's outputs, and compare every stage."""
+    cam = S.parse_camera(camjson)
+    dsc = rnd.upload(data)
+    rays = refgpu.generate(cam, w, h)
+    n = len(rays)
+    seeds = R.default_seeds(n)
+    colors = np.ones((n, 4), np.float32)
+    hits = np.zeros(n, L.HIT)
+    for b in range(depth):
+        live = (rays["origin"][:, 3].view(np.int32) & np.int32(-16777216)) == 0
+        ref_hits = refgpu.intersect(data, rays, hits=hits)
+        mine_hits = R.records(rnd.intersect(dsc, R.to_device(rays, rnd.device), hits=R.to_device(hits, rnd.device),
+                                            mode=mode), L.HIT)
+        hit_fields_equal(mine_hits, ref_hits, live, "bounce%d.hit" % b, check_tri=(mode == L.MODE_NOPRUNE))
+        hits = ref_hits
+        r_rays, r_col, r_seed = refgpu.shade(data, rays, hits, colors, seeds, depth)
+        d_rays = R.to_device(rays, rnd.device)
+        d_col = torch.from_numpy(colors.copy()).to(rnd.device)
+        d_seed = torch.from_numpy(seeds.view(np.int32).copy()).to(rnd.device)
+        rnd.shade(dsc, d_rays, R.to_device(hits, rnd.device), d_col, d_seed, depth)
+        m_rays = R.records(d_rays, L.RAY)
+        assert_bits_equal(d_col.cpu().numpy(), r_col, "bounce%d.color" % b)
+        assert_bits_equal(d_seed.cpu().numpy().view(np.uint32), r_seed, "bounce%d.seed" % b)
+        ray_fields_equal(m_rays, r_rays, "bounce%d.ray" % b)
+        rays, colors, seeds = r_rays, r_col, r_seed
+    dsc.close()
+
+
+@needs_ref
+@pytest.mark.parametrize("mode", [L.MODE_EXACT, L.MODE_NOPRUNE])
+@pytest.mark.parametrize("name,getter,camjson", SCENES)
+def test_bounce_chain_bitexact(rnd, name, getter, camjson, mode):
+    _bounce_chain(rnd, getter(), camjson, 48, 40, 6, mode)
+
+
+@needs_ref
+@pytest.mark.parametrize("max_attempt", [4, 16])
+def test_accumulate_bitexact(rnd, max_attempt):
+    w, h = 32, 16
+    rng = np.random.default_rng(1)
+    hist = np.zeros((w * h, 4), np.float32)
+    count = np.zeros(w * h, np.int32)
+    dh = torch.zeros((w * h, 4), dtype=torch.float32, device=rnd.device)
+    dn = torch.zeros(w * h, dtype=torch.int32, device=rnd.device)
+    for f in range(max_attempt + 3):
+        col = rng.exponential(1.0, (w * h, 4)).astype(np.float32)
+        col[rng.random(w * h) < 0.3] = 0.0
+        col[:, 3] = 0.0
+        rc, hist, count = refgpu.accumulate(col, hist, count, w, h, max_attempt)
+        dc = torch.from_numpy(col).to(rnd.device)
+        rnd.accumulate(dc, dh, dn, max_attempt)
+        assert_bits_equal(dc.cpu().numpy(), rc, "display")
+        assert_bits_equal(dh.cpu().numpy(), hist, "history")
+        assert_bits_equal(dn.cpu().numpy(), count, "count")
+
+
+def _render_both(rnd, data, camjson, w, h, depth, frames, attempt, mode=L.MODE_EXACT, **kw):
+    cam = S.parse_camera(camjson)
+    seeds = R.default_seeds(w * h)
+    ref_hist, ref_count, ref_seeds = refgpu.render(data, cam, w, h, depth, frames, attempt, seeds)
+    dsc = rnd.upload(data)
+    st = rnd.new_state(w, h, seeds)
+    rnd.render_frames(dsc, cam, st, depth, attempt, frames, mode=mode, **kw)
+    torch.cuda.synchronize()
+    out = st.hist.cpu().numpy(), st.count.cpu().numpy(), st.seeds_np()
+    dsc.close()
+    return out, (ref_hist, ref_count, ref_seeds)
+
+
+@needs_ref
+@pytest.mark.parametrize("name,getter,camjson,depth", [("cbox", scenes.cbox, scenes.CBOX_CAM, 4),
+                                                       ("cbox_diffuse", scenes.cbox_diffuse, scenes.CBOX_CAM, 8),
+                                                       ("mis", scenes.mis, scenes.MIS_CAM, 12)])
+def test_render_frames_bitexact(rnd, name, getter, camjson, depth):
+    (h_, c_, s_), (rh, rc, rs) = _render_both(rnd, getter(), camjson, 64, 64, depth, 6, 4)
+    assert_bits_equal(c_, rc, "count")
+    assert_bits_equal(s_, rs, "seeds")
+    assert_bits_equal(h_, rh, "hist")
+
+
+@needs_ref
+def test_render_frames_chunked_and_striped_bitexact(rnd):
+    """Frames split across launches and rows split into stripes (the multi-GPU
+    partition, run sequentially here) change nothing."""
+    data, cam = scenes.cbox(), S.parse_camera(scenes.CBOX_CAM)
+    w, h, depth, frames, attempt = 48, 40, 5, 7, 4
+    seeds = R.default_seeds(w * h)
+    rh, rc, rs = refgpu.render(data, cam, w, h, depth, frames, attempt, seeds)
+    dsc = rnd.upload(data)
+    for stripes in (1, 3):
+        st = rnd.new_state(w, h, seeds)
+        for k in range(stripes):
+            for f0, nf in ((0, 2), (2, 5)):
+                rnd.render_frames(dsc, cam, st, depth, attempt, nf, frame_begin=f0, stripe_rows=8, stripe_index=k,
+                                  stripe_count=stripes, frames_per_launch=3)
+        torch.cuda.synchronize()
+        assert_bits_equal(st.count.cpu().numpy(), rc, "count/%d" % stripes)
+        assert_bits_equal(st.seeds_np(), rs, "seeds/%d" % stripes)
+        assert_bits_equal(st.hist.cpu().numpy(), rh, "hist/%d" % stripes)
+    dsc.close()
+
+
+def test_exact_equals_noprune_full_size(rnd):
+    """Size-independent property at a C2-like configuration: the pruned
+    traversal reproduces the exhaustive reference traversal exactly."""
+    data, cam = scenes.cbox_diffuse(), S.parse_camera(scenes.CBOX_CAM)
+    w = h = 256
+    seeds = R.default_seeds(w * h)
+    dsc = rnd.upload(data)
+    outs = []
+    for mode in (L.MODE_EXACT, L.MODE_NOPRUNE):
+        st = rnd.new_state(w, h, seeds)
+        rnd.render_frames(dsc, cam, st, 8, 256, 4, mode=mode)
+        torch.cuda.synchronize()
+        outs.append((st.hist.cpu().numpy(), st.count.cpu().numpy(), st.seeds_np()))
+    for a, b, what in zip(outs[0], outs[1], ("hist", "count", "seeds")):
+        assert_bits_equal(a, b, what)
+    dsc.close()

@@ -1,0 +1,48 @@
+"""Quick single-GPU timing of the fused path on the C2 configuration."""
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import torch  # noqa: E402
+
+from montecarlopathtracing_amd import _lib as L  # noqa: E402
+from montecarlopathtracing_amd import render as R  # noqa: E402
+from montecarlopathtracing_amd import scene as S  # noqa: E402
+from tests import scenes  # noqa: E402
+
+
+def main():
+    frames = int(sys.argv[1]) if len(sys.argv) > 1 else 16
+    w = h = int(sys.argv[2]) if len(sys.argv) > 2 else 1024
+    depth = 8
+    which = sys.argv[3] if len(sys.argv) > 3 else "cbox_diffuse"
+    data = getattr(scenes, which)()
+    camj = scenes.MIS_CAM if which == "mis" else scenes.CBOX_CAM
+    cam = S.parse_camera(camj)
+    r = R.Renderer(0)
+    dsc = r.upload(data)
+    for mode in (L.MODE_EXACT,):
+        for stats in (True, False):
+            r.set_stats(stats)
+            st = r.new_state(w, h)
+            r.render_frames(dsc, cam, st, depth, 1 << 20, 1, mode=mode)  # warm
+            torch.cuda.synchronize()
+            t0 = time.time()
+            r.render_frames(dsc, cam, st, depth, 1 << 20, frames, mode=mode)
+            torch.cuda.synchronize()
+            dt = time.time() - t0
+            s = r.stats()
+            nominal = w * h * frames * depth / dt / 1e6
+            print("mode=%d stats=%d frames=%d %.3fs nominal %.1f Msamples/s kernel_ms=%.1f launches=%d" % (
+                mode, stats, frames, dt, nominal, s["kernel_ms"], s["launches"]))
+            if stats:
+                seg = s["segments"]
+                print("   segments %.3g (%.2f/path) nodes/seg %.2f tris/seg %.2f bad %d active Mseg/s %.1f" % (
+                    seg, seg / (w * h * frames), s["node_visits"] / seg, s["tri_tests"] / seg, s["bad_material"],
+                    seg / dt / 1e6))
+
+
+if __name__ == "__main__":
+    main()
