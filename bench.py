@@ -1,0 +1,214 @@
+#!/usr/bin/env python3
+"""Headline benchmark: nominal Msamples/s (pixels x frames x bounces / s) of the
+fused HIP path-tracing loop on BASELINE.json configs[1] (C2): Scene/cbox,
+1024x1024 per GPU, 8 bounces, diffuse-only BRDF.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    torchrun --nproc-per-node N ... bench.py --gpus N       (one process per GPU)
+
+A step = one frame: every pixel of the rank's image tile traces one sample of
+up to 8 bounces and is accumulated (OpenCL::update + ColorOut once).  Scaling
+is weak: each rank owns a 1024x1024 tile of a 1024 x (1024*N) image (row
+stripes interleaved across ranks); no collective runs inside the timed region.
+The timed region is bracketed by barrier + synchronize and the max over ranks
+is reported.  Scene data, seeds and accumulators are resident in HBM before
+timing starts.
+
+Also reported (rank 0, N=1 only for cpu_baseline):
+  roofline     — SURVEY.md §8(d): algorithmic bytes per active segment
+                 B_seg = 328 + 64 (E_node + E_tri), E_* measured per config by
+                 the CPU oracle's t-pruned left-first traversal (cached in
+                 profiles/e_counts.json); achieved = B_seg x segments per launch
+                 / average launch time (HIP events on the launch stream).
+  cpu_baseline — the CPU oracle (plain-C restatement of the reference
+                 algorithm, OpenMP) on a bounded pixel sample of the same
+                 workload, on this host's cores.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+W = 1024
+H_PER_GPU = 1024
+DEPTH = 8
+STRIPE_ROWS = 16
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+METRIC = "Msamples/s (rays traced x bounces / s) at 1024x1024"
+
+
+def dist_env():
+    ws = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    return ws, rank, local
+
+
+def load_scene():
+    from montecarlopathtracing_amd import scene as S
+    return S.SceneData.from_obj(os.path.join(ROOT, "scenes/cbox/"), "cbox.obj", material_override=S.diffuse_only)
+
+
+CBOX_CAM = {"position": [278, 273, -800], "lookat": [278, 273, -799], "up": [0, 1, 0], "fov": 39.3077}
+
+
+def e_counts():
+    """E_node / E_tri (per active segment) of the t-pruned, left-first
+    reference traversal, measured once by the CPU oracle
+    (tests/measure_e_counts.py) and committed in profiles/e_counts.json."""
+    try:
+        with open(os.path.join(ROOT, "profiles", "e_counts.json")) as fh:
+            return json.load(fh).get("C2")
+    except (OSError, ValueError):
+        return None
+
+
+def default_seeds(n):
+    from montecarlopathtracing_amd.render import default_seeds as ds
+    return ds(n)
+
+
+def cpu_baseline(data, cam, h_img, target_s=12.0):
+    """The CPU oracle on a bounded sample: every k-th pixel of the same image,
+    same depth, frames scaled so the sample takes ~target_s seconds."""
+    from tests import oracle as O
+    if not O.available():
+        return None
+    threads = max(1, min(16, os.cpu_count() or 1))
+    seeds = default_seeds(W * h_img)
+    stride = 61
+    px = np.arange(0, W * h_img, stride, dtype=np.int32)
+    t0 = time.time()
+    O.render(data, cam, W, h_img, DEPTH, 1, 1 << 20, seeds, pixels=px[:2048], threads=threads)
+    probe = max(time.time() - t0, 1e-3)
+    frames = int(max(1, min(64, target_s / (probe * len(px) / 2048.0))))
+    t0 = time.time()
+    _, _, _, st = O.render(data, cam, W, h_img, DEPTH, frames, 1 << 20, seeds, pixels=px, threads=threads)
+    dt = time.time() - t0
+    return {"value": len(px) * frames * DEPTH / dt / 1e6, "unit": "Msamples/s", "cores": threads,
+            "kind": "port",
+            "sample": "every %dth pixel (%d px) of the 1024x1024 C2 image x %d frames x depth %d, %.1f s; "
+                      "oracle/mcpt_oracle.c exhaustive reference traversal, %d OpenMP threads" % (
+                          stride, len(px), frames, DEPTH, dt, threads),
+            "active_Msegments_per_s": float(st[0]) / dt / 1e6}
+
+
+def load_traffic():
+    """HBM bytes per launch from the committed rocprofv3 PMC summary, if any."""
+    path = os.path.join(ROOT, "profiles", "pmc_summary.json")
+    try:
+        with open(path) as fh:
+            j = json.load(fh)
+        return j.get("hbm_bytes_per_launch")
+    except (OSError, ValueError):
+        return None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=64)
+    ap.add_argument("--warmup", type=int, default=4)
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--frames-per-launch", type=int, default=16)
+    args = ap.parse_args()
+
+    ws, rank, local = dist_env()
+    n = max(ws, 1)
+    if ws > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    from montecarlopathtracing_amd import _lib as L
+    from montecarlopathtracing_amd import render as R
+    from montecarlopathtracing_amd import scene as S
+
+    h_img = H_PER_GPU * n
+    data = load_scene()
+    cam = S.parse_camera(CBOX_CAM)
+    rnd = R.Renderer(local if ws > 1 else 0)
+    dsc = rnd.upload(data)
+    seeds = default_seeds(W * h_img)
+    st = rnd.new_state(W, h_img, seeds)
+    kw = dict(stripe_rows=STRIPE_ROWS, stripe_index=rank, stripe_count=n, frames_per_launch=args.frames_per_launch)
+    attempt = 1 << 30  # accumulate every frame (the reference's MAX_ATTEMPT cap never binds here)
+
+    # warmup (untimed)
+    if args.warmup > 0:
+        rnd.render_frames(dsc, cam, st, DEPTH, attempt, args.warmup, **kw)
+    # snapshot for the segment-count replay
+    snap = (st.seeds.clone(), st.hist.clone(), st.count.clone(), st.frames_done)
+    torch.cuda.synchronize()
+    if ws > 1:
+        torch.distributed.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    rnd.render_frames(dsc, cam, st, DEPTH, attempt, args.steps, **kw)
+    torch.cuda.synchronize()
+    if ws > 1:
+        torch.distributed.barrier()
+    elapsed = time.perf_counter() - t0
+    kst = rnd.stats()
+    kernel_ms, launches = kst["kernel_ms"], max(kst["launches"], 1)
+    if ws > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=rnd.device)
+        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    # replay the same frames with counters on (deterministic: same segments)
+    st.seeds.copy_(snap[0]), st.hist.copy_(snap[1]), st.count.copy_(snap[2])
+    st.frames_done = snap[3]
+    rnd.set_stats(True)
+    rnd.render_frames(dsc, cam, st, DEPTH, attempt, args.steps, **kw)
+    cst = rnd.stats()
+    rnd.set_stats(False)
+    segments = cst["segments"]
+
+    total_samples = float(W * H_PER_GPU) * n * args.steps * DEPTH
+    value = total_samples / elapsed / 1e6
+    out = None
+    if rank == 0:
+        ec = e_counts()
+        roof = None
+        if ec:
+            b_seg = 328.0 + 64.0 * (ec["E_node"] + ec["E_tri"])
+            seg_per_launch = segments / float(launches)
+            avg_launch_s = kernel_ms / 1e3 / launches
+            achieved = b_seg * seg_per_launch / avg_launch_s / 1e9
+            traffic = load_traffic()
+            roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                    "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                    "B_seg": round(b_seg, 1), "E_node": round(ec["E_node"], 3), "E_tri": round(ec["E_tri"], 3),
+                    "segments_per_launch": int(seg_per_launch), "avg_launch_ms": round(avg_launch_s * 1e3, 3),
+                    "kernel": "k_render<0,false>",
+                    "kernel_node_fetches_per_seg": round(cst["node_visits"] / max(segments, 1), 3),
+                    "kernel_tri_tests_per_seg": round(cst["tri_tests"] / max(segments, 1), 3)}
+        cpu = None
+        if n == 1 and not args.no_cpu:
+            cpu = cpu_baseline(data, cam, h_img)
+        out = {"metric": METRIC, "value": round(value, 2), "unit": "Msamples/s", "n_gpus": n, "steps": args.steps,
+               "warmup": args.warmup, "ms_per_step": round(elapsed * 1e3 / args.steps, 4),
+               "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+               "data": "synthetic seeds; Scene/cbox geometry recovered from the reference's cbox.mb",
+               "config": {"workload": "C2: cbox 1024x1024/GPU, 8 bounces, diffuse-only, 1 sample/pixel/step",
+                          "width": W, "height_per_gpu": H_PER_GPU, "max_depth": DEPTH,
+                          "parallelism": "row-stripe tiles x%d" % n, "mode": "exact"},
+               "active_Msegments_per_s": round(segments * n / elapsed / 1e6, 2),
+               "roofline": roof, "cpu_baseline": cpu}
+        print(json.dumps(out), flush=True)
+    dsc.close()
+    rnd.close()
+    if ws > 1:
+        torch.distributed.destroy_process_group()
+    return out
+
+
+if __name__ == "__main__":
+    main()

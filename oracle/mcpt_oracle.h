@@ -1,0 +1,55 @@
+/* mcpt_oracle.h — TEST INFRASTRUCTURE ONLY (tests/, __graft_entry__.smoke()
+ * and bench.py's cpu_baseline leg).  Never linked into libmcpt_hip.so.
+ *
+ * A plain-C CPU restatement of the reference's per-sample path (records from
+ * include/mcpt_hip.h, byte-identical to MCPT/objdef.h).  Each function cites
+ * the reference lines it restates.  Floating point: IEEE binary32, with an
+ * explicit fmaf() exactly where OpenCL's default FP_CONTRACT fuses an
+ * expression in the reference kernels, libm for the transcendentals; the
+ * GPU's OpenCL built-ins (hardware rcp/rsq/sqrt, ocml cos/sin/pow) round some
+ * results differently by an ulp, so kernel outputs agree to a few ulp and
+ * chaotic paths diverge — tests compare with stated tolerances.
+ * Pinned against the reference kernels' own outputs: tests/golden/.
+ */
+#ifndef MCPT_ORACLE_H
+#define MCPT_ORACLE_H
+#include <stdint.h>
+
+#include "../include/mcpt_hip.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+int oracle_parse_camera(const double pos[3], const double look[3], const double up[3], double fov, mcpt_camera *out);
+int oracle_pack_triangles(mcpt_triangle *tris, const int32_t *mat_index, int64_t n);
+int oracle_build_hlbvh(const mcpt_triangle *tris, int64_t n, mcpt_bvh_node *nodes);
+void oracle_generate(const mcpt_camera *cam, int32_t w, int32_t h, mcpt_ray *rays);
+void oracle_intersect(const mcpt_triangle *tris, const mcpt_bvh_node *nodes, const mcpt_ray *rays, int64_t n,
+                      mcpt_hit *hits, float tmin);
+void oracle_shade(const mcpt_material *mats, mcpt_ray *rays, const mcpt_hit *hits, float *colors, uint32_t *seeds,
+                  int64_t n, int32_t max_depth);
+void oracle_accumulate(float *colors, float *hist, int32_t *count, int64_t n, int32_t max_attempt);
+/* Whole frame loop per pixel (OpenCLApp.cpp:57-82 + colorout.cpp:40-73) over
+ * `frames` frames starting at frame index frame_begin, OpenMP over pixels
+ * with `threads` threads (<= 0: all).  stats[4] (optional): segments, node
+ * visits, triangle tests, unknown-material hits. */
+void oracle_render(const mcpt_camera *cam, const mcpt_triangle *tris, const mcpt_bvh_node *nodes,
+                   const mcpt_material *mats, int32_t w, int32_t h, int32_t max_depth, int32_t frame_begin,
+                   int32_t frames, int32_t max_attempt, uint32_t *seeds, float *hist, int32_t *count,
+                   int32_t threads, uint64_t *stats);
+/* Same, restricted to a pixel subset (indices into W*H), for bounded samples. */
+void oracle_render_pixels(const mcpt_camera *cam, const mcpt_triangle *tris, const mcpt_bvh_node *nodes,
+                          const mcpt_material *mats, int32_t w, int32_t h, const int32_t *pixels, int64_t npix,
+                          int32_t max_depth, int32_t frame_begin, int32_t frames, int32_t max_attempt,
+                          uint32_t *seeds, float *hist, int32_t *count, int32_t threads, uint64_t *stats);
+/* Counting mode for SURVEY §8(d)'s E_node/E_tri: 1 = t-pruned traversal
+ * (skip a node whose box starts beyond the current hit).  Default 0 =
+ * the reference's exhaustive traversal. */
+void oracle_set_prune(int on);
+int64_t oracle_encode_hdr(int32_t w, int32_t h, const float *rgba, int32_t flip, uint8_t *out, int64_t cap);
+
+#ifdef __cplusplus
+}
+#endif
+#endif
