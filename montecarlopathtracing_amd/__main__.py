@@ -1,0 +1,64 @@
+"""Command line: render a reference config.json on the GPU(s) and write the .hdr.
+
+    python -m montecarlopathtracing_amd [config.json] [--configid N] [--out DIR]
+    torchrun --nproc-per-node 8 -m montecarlopathtracing_amd config.json   (row-stripe tiles)
+"""
+import argparse
+import os
+import sys
+import time
+
+
+def main(argv=None):
+    ap = argparse.ArgumentParser(prog="montecarlopathtracing_amd")
+    ap.add_argument("config", nargs="?", default="config.json")
+    ap.add_argument("--configid", type=int, default=None)
+    ap.add_argument("--out", default=".")
+    ap.add_argument("--frames", type=int, default=None, help="override attempt+1 frames")
+    a = ap.parse_args(argv)
+    ws = int(os.environ.get("WORLD_SIZE", "1"))
+    if ws > 1:
+        return _main_dist(a)
+    from .app import App
+    app = App(a.config, a.configid, out_dir=a.out)
+    t0 = time.time()
+    if a.frames:
+        app.update(a.frames)
+        path = app.output_picture()
+    else:
+        path = app.run()
+    print("wrote %s (%dx%d, %d frames, %.2f s)" % (path, app.w, app.h, app.attempt_count, time.time() - t0))
+    return 0
+
+
+def _main_dist(a):
+    import torch
+    import torch.distributed as dist
+
+    from . import config as C
+    from . import dist as D
+    from . import render as R
+    from . import scene as S
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    cfg = C.Config(a.config, a.configid)
+    root = os.path.dirname(os.path.abspath(a.config))
+    over = S.diffuse_only if cfg.entry.get("materials") == "diffuse_only" else None
+    data = S.SceneData.from_obj(os.path.join(root, cfg.GETDIRECTORY()), cfg.GETOBJNAME(), over)
+    rnd = R.Renderer(local)
+    sc = rnd.upload(data)
+    w, h = cfg.WIDTH(), cfg.HEIGHT()
+    frames = a.frames or cfg.MAXATTEPMT() + 1
+    out = D.render_distributed(rnd, sc, S.parse_camera(cfg.GETCAMERA()), w, h, cfg.MAXDEPTH(), cfg.MAXATTEPMT(),
+                               frames, R.default_seeds(w * h))
+    if dist.get_rank() == 0:
+        path = os.path.join(a.out, cfg.GETOBJNAME() + ".hdr")
+        S.write_hdr(path, out[0].reshape(h, w, 4))
+        print("wrote", path)
+    dist.destroy_process_group()
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

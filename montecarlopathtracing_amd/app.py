@@ -1,0 +1,85 @@
+"""The reference's application loop on the HIP path: OpenCL::init/update
+(MCPT/OpenCLApp.cpp:36-82) + ColorOut (MCPT/colorout.cpp:31-73), headless.
+
+    app = App("config.json")      # config.json of the reference (configid selects the entry)
+    app.run()                     # attempt+1 frames accumulated, then <objname>.hdr
+
+Frame semantics kept: frames 0..attempt run the history kernel (attemptCount
+<= MAX_ATTEMPT), the .hdr is written once after that from the accumulated
+frameBuffer, vertically flipped like stbi_flip_vertically_on_write(true).
+"""
+import os
+
+import numpy as np
+
+from . import config as C
+from . import scene as S
+
+
+class App:
+    def __init__(self, cfg, configid=None, device=0, seeds=None, out_dir=".", root=None,
+                 material_override=None):
+        self.cfg = cfg if isinstance(cfg, C.Config) else C.Config(cfg, configid)
+        if self.cfg.TESTBVH() or self.cfg.TESTALL():
+            raise ValueError("testbvh/testall modes are BVH-quality tools, not the render path")
+        if not self.cfg.USEOPENCL():
+            raise ValueError('config has "opencl": false — the reference throws "Not Implemented" here')
+        self.root = root if root is not None else (os.path.dirname(os.path.abspath(cfg)) if isinstance(cfg, str) else ".")
+        self.device = device
+        self.seeds = seeds
+        self.out_dir = out_dir
+        self.material_override = material_override
+        if material_override is None and self.cfg.entry.get("materials") == "diffuse_only":
+            self.material_override = S.diffuse_only
+        self.attempt_count = 0
+        self.dumped = None
+        self._init = False
+
+    def init(self):
+        """OpenCL::init: load OBJ, build scene, camera, buffers (OpenCLApp.cpp:36-55)."""
+        from . import render as R
+        cam = self.cfg.GETCAMERA()
+        res = cam.get("resolution", [self.cfg.WIDTH(), self.cfg.HEIGHT()])
+        if [int(res[0]), int(res[1])] != [self.cfg.WIDTH(), self.cfg.HEIGHT()]:
+            # the reference sizes rays by camera.resolution but colour by width/height
+            # (raygeneration.cpp:51-56 vs OpenCLApp.cpp:38-51); a mismatch is undefined there
+            raise ValueError("camera.resolution must equal width/height")
+        self.w, self.h = self.cfg.WIDTH(), self.cfg.HEIGHT()
+        directory = os.path.join(self.root, self.cfg.GETDIRECTORY())
+        if not directory.endswith("/"):
+            directory += "/"
+        self.data = S.SceneData.from_obj(directory, self.cfg.GETOBJNAME(), self.material_override)
+        self.camera = S.parse_camera(cam)
+        self.renderer = R.Renderer(self.device)
+        self.scene = self.renderer.upload(self.data)
+        self.state = self.renderer.new_state(self.w, self.h, self.seeds)
+        self._init = True
+
+    def update(self, frames=1):
+        """`frames` display frames of OpenCL::update; dumps the .hdr once the
+        history has taken attempt+1 frames (colorout.cpp:56-68)."""
+        if not self._init:
+            self.init()
+        att = self.cfg.MAXATTEPMT()
+        todo = frames
+        while todo > 0:
+            n = todo if self.attempt_count > att else min(todo, att + 1 - self.attempt_count)
+            self.renderer.render_frames(self.scene, self.camera, self.state, self.cfg.MAXDEPTH(), att, n)
+            self.attempt_count += n
+            todo -= n
+            if self.attempt_count > att and self.dumped is None:
+                self.dumped = self.output_picture()
+        return self.state
+
+    def output_picture(self, path=None):
+        """ThirdPartyWrapper::outputPicture(<objname>.hdr, frameBuffer)."""
+        path = path or os.path.join(self.out_dir, self.cfg.GETOBJNAME() + ".hdr")
+        S.write_hdr(path, self.state.image(), flip=True)
+        return path
+
+    def run(self):
+        self.update(self.cfg.MAXATTEPMT() + 1)
+        return self.dumped
+
+    def image(self):
+        return self.state.image()
