@@ -133,6 +133,9 @@ typedef struct mcpt_stats {
   double   kernel_ms;               /* device time of the last render call   */
   int32_t  launches;                /* kernel launches of the last render call */
   int32_t  pad;
+  uint64_t wave_node_phases;        /* wave-level node steps (SIMT efficiency = */
+  uint64_t wave_leaf_phases;        /*  node_visits / (64 * wave_node_phases)) */
+  uint64_t wave_shade_phases;
 } mcpt_stats;
 
 /* ------------------------------------------------------- version / errors */

@@ -11,7 +11,7 @@ import os
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "lib", "libmcpt_hip.so")
+LIB_PATH = os.environ.get("MCPT_LIB_OVERRIDE") or os.path.join(_HERE, "lib", "libmcpt_hip.so")  # override: tuning sweeps only
 
 # ------------------------------------------------ record dtypes (objdef.h)
 CAMERA = np.dtype([("center", "<f4", 4), ("direction", "<f4", 4), ("up", "<f4", 4),
@@ -42,7 +42,9 @@ class RenderParams(ctypes.Structure):
 class Stats(ctypes.Structure):
     _fields_ = [("segments", ctypes.c_uint64), ("node_visits", ctypes.c_uint64),
                 ("tri_tests", ctypes.c_uint64), ("bad_material", ctypes.c_uint64),
-                ("kernel_ms", ctypes.c_double), ("launches", ctypes.c_int32), ("pad", ctypes.c_int32)]
+                ("kernel_ms", ctypes.c_double), ("launches", ctypes.c_int32), ("pad", ctypes.c_int32),
+                ("wave_node_phases", ctypes.c_uint64), ("wave_leaf_phases", ctypes.c_uint64),
+                ("wave_shade_phases", ctypes.c_uint64)]
 
 
 class MCPTError(RuntimeError):

@@ -19,6 +19,9 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <climits>
+#include <cstdio>
+#include <cstdlib>
 #include <cmath>
 #include <cstring>
 #include <string>
@@ -28,6 +31,10 @@
 #include "mcpt_refmath.h"
 
 using namespace mcpt;
+
+#ifndef MCPT_WAVES_PER_SIMD
+#define MCPT_WAVES_PER_SIMD 4  // k_render occupancy target (tools/sweep_waves.sh)
+#endif
 
 namespace mcpt {
 int fail(int code, const std::string &msg);  // mcpt_host.cpp
@@ -77,7 +84,7 @@ struct mcpt_scene {
 struct mcpt_ctx {
   int device;
   bool stats_on = false;
-  unsigned long long *d_stats = nullptr;  // segments, nodes, tris, bad
+  unsigned long long *d_stats = nullptr;  // segments, nodes, tris, bad, wave T/L/S phases
   mcpt_stats last;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
 };
@@ -126,6 +133,14 @@ __device__ inline void test_tri(const DevTri *__restrict__ tris, int32_t id, f3 
 // Left-first DFS of objdef.h:240-275.  PRUNE skips a child whose box starts
 // farther than the current hit plus a margin: every triangle inside it would
 // have t > hit.t and could not replace the hit.
+//
+// SIMT shape ("while-while", Aila & Laine 2009): the inner loop walks internal
+// nodes until EVERY lane of the wave holds a leaf (or is done); then all lanes
+// with a leaf run the Cramer test together.  Each lane still tests its
+// triangles in exactly the reference's DFS order.
+constexpr int32_t kDone = INT32_MIN;       // traversal finished
+constexpr int32_t kPop = INT32_MIN + 1;    // take the next entry from the stack
+
 template <bool PRUNE, bool LITERAL>
 __device__ inline Trace traverse(const SceneView &S, f3 o, f3 d, float tmin, int32_t *stk, int stride) {
   Trace tr;
@@ -138,50 +153,39 @@ __device__ inline Trace traverse(const SceneView &S, f3 o, f3 d, float tmin, int
   rinv.x = __builtin_amdgcn_rcpf(d.x);
   rinv.y = __builtin_amdgcn_rcpf(d.y);
   rinv.z = __builtin_amdgcn_rcpf(d.z);
-  if (!slab_pass(box_test<LITERAL>(S.root_min.xyz, S.root_max.xyz, o, d, rinv), tmin)) return tr;
-  if (S.root_leaf >= 0) {
-    test_tri(S.tris, S.root_leaf, o, d, tmin, tr);
-    return tr;
-  }
+  int32_t cur;  // >= 0 internal node, kDone, or ~triangle (a leaf waiting for its test)
+  if (!slab_pass(box_test<LITERAL>(S.root_min.xyz, S.root_max.xyz, o, d, rinv), tmin))
+    cur = kDone;
+  else
+    cur = S.root_leaf >= 0 ? ~S.root_leaf : 0;
   const DevNode *__restrict__ nodes = S.nodes;
-  int32_t node = 0;
   int sp = 0;
-  for (;;) {
-    const DevNode N = nodes[node];
-    tr.nodes++;
-    f3 lmin = N.a.xyz, lmax = (f3){N.a.w, N.b.x, N.b.y};
-    f3 rmin = (f3){N.b.z, N.b.w, N.c.x}, rmax = N.c.yzw;
-    BoxT bl = box_test<LITERAL>(lmin, lmax, o, d, rinv);
-    BoxT br = box_test<LITERAL>(rmin, rmax, o, d, rinv);
-    bool hl = slab_pass(bl, tmin), hr = slab_pass(br, tmin);
-    if (PRUNE) {
-      const float lim = tr.t + S.prune_margin;
-      hl = hl && !(bl.tnear > lim);
-      hr = hr && !(br.tnear > lim);
+  while (cur != kDone) {
+    // ---- walk internal nodes until this lane holds a leaf or is done
+    while (cur >= 0) {
+      const DevNode N = nodes[cur];
+      tr.nodes++;
+      f3 lmin = N.a.xyz, lmax = (f3){N.a.w, N.b.x, N.b.y};
+      f3 rmin = (f3){N.b.z, N.b.w, N.c.x}, rmax = N.c.yzw;
+      BoxT bl = box_test<LITERAL>(lmin, lmax, o, d, rinv);
+      BoxT br = box_test<LITERAL>(rmin, rmax, o, d, rinv);
+      bool hl = slab_pass(bl, tmin), hr = slab_pass(br, tmin);
+      if (PRUNE) {
+        const float lim = tr.t + S.prune_margin;
+        hl = hl && !(bl.tnear > lim);
+        hr = hr && !(br.tnear > lim);
+      }
+      if (hl && hr) stk[(sp++) * stride] = N.right;  // reference: push right, descend left
+      cur = hl ? N.left : (hr ? N.right : kPop);
+      if (cur == kPop) cur = sp == 0 ? kDone : stk[(--sp) * stride];
     }
-    int32_t next = -1;
-    if (hl) {
-      if (hr) stk[(sp++) * stride] = N.right;  // reference: push right, descend left
-      if (N.left < 0)
-        test_tri(S.tris, ~N.left, o, d, tmin, tr);
-      else
-        next = N.left;
-    } else if (hr) {
-      if (N.right < 0)
-        test_tri(S.tris, ~N.right, o, d, tmin, tr);
-      else
-        next = N.right;
+    // ---- all lanes: test the pending leaf, then continue from the stack
+    if (cur != kDone) {
+      test_tri(S.tris, ~cur, o, d, tmin, tr);
+      cur = sp == 0 ? kDone : stk[(--sp) * stride];
     }
-    while (next < 0) {  // pop: leaves are tested as they come off the stack
-      if (sp == 0) return tr;
-      int32_t x = stk[(--sp) * stride];
-      if (x < 0)
-        test_tri(S.tris, ~x, o, d, tmin, tr);
-      else
-        next = x;
-    }
-    node = next;
   }
+  return tr;
 }
 
 // --------------------------------------------------------------- generateRay
@@ -330,6 +334,7 @@ struct RenderArgs {
   int32_t stripe_rows, stripe_index, stripe_count;
   int32_t max_depth, max_attempt, frame_begin, frames;
   int32_t stack_depth;
+  int32_t th_leaf, th_shade;  // lanes waiting before the L / S phase runs
 };
 
 __device__ inline int32_t global_row(int32_t lr, const RenderArgs &A) {
@@ -339,8 +344,19 @@ __device__ inline int32_t global_row(int32_t lr, const RenderArgs &A) {
 
 constexpr float kTmin = 0.001f;  // host EPSILON passed as tmin (oclbasic.h:193, scenebuild.cpp:125)
 
+// The fused kernel is a per-wave state machine.  Every lane is in one of
+//   T: walking internal BVH nodes (cur >= 0)
+//   L: holding a leaf whose triangle must be tested (cur = ~tri)
+//   S: segment traced (cur == kDone): shade, accumulate, start the next segment
+// and each loop iteration runs one T step for the T lanes, then the L phase
+// and the S phase only when enough lanes are waiting for them (or nothing
+// else can run).  Expensive phases therefore execute with most of the wave
+// active instead of once per diverging lane.  Each lane's own
+// sequence of operations is exactly the reference's, so results are unchanged.
 template <int MODE, bool STATS>
-__global__ void __launch_bounds__(64) k_render(RenderArgs A) {
+__global__ void __launch_bounds__(64, MCPT_WAVES_PER_SIMD) k_render(RenderArgs A) {
+  constexpr bool PRUNE = MODE != MCPT_MODE_NOPRUNE;
+  constexpr bool LIT = MODE == MCPT_MODE_NOPRUNE;
   extern __shared__ int32_t lds_stack[];
   const int lane = threadIdx.x;
   int32_t *stk = lds_stack + lane;  // column-major [depth][64]: conflict-free
@@ -351,6 +367,7 @@ __global__ void __launch_bounds__(64) k_render(RenderArgs A) {
   const int32_t y = global_row(lr, A);
   if (y >= A.H) return;
   const int32_t pid = y * A.W + x;
+  const SceneView &S = A.S;
 
   uint32_t seed = A.seeds[pid];
   f4 hist = A.hist[pid];
@@ -359,46 +376,108 @@ __global__ void __launch_bounds__(64) k_render(RenderArgs A) {
   gen_ray(A.cam, (uint32_t)x, (uint32_t)y, (uint32_t)A.W, (uint32_t)A.H, o0, d0);
 
   unsigned long long n_seg = 0, n_nodes = 0, n_tests = 0, n_bad = 0;
+  unsigned long long w_t = 0, w_l = 0, w_s = 0;
   int32_t f = 0;
+  bool live = A.frames > 0;
   f4 o = o0, d = d0;
   f4 color = (f4){1.0f, 1.0f, 1.0f, 1.0f};
-  while (f < A.frames) {
-    // intersect.cl: trace one segment
-    Trace tr = MODE == MCPT_MODE_NOPRUNE ? traverse<false, true>(A.S, o.xyz, d.xyz, kTmin, stk, 64)
-                                         : traverse<true, false>(A.S, o.xyz, d.xyz, kTmin, stk, 64);
-    if (STATS) {
-      n_seg++;
-      n_nodes += tr.nodes;
-      n_tests += tr.tests;
+  f3 rinv;
+  float best_t;
+  int32_t best_tri, cur, sp;
+  auto begin_segment = [&]() {
+    rinv.x = __builtin_amdgcn_rcpf(d.x);
+    rinv.y = __builtin_amdgcn_rcpf(d.y);
+    rinv.z = __builtin_amdgcn_rcpf(d.z);
+    best_t = kFltMax;
+    best_tri = -1;
+    sp = 0;
+    if (slab_pass(box_test<LIT>(S.root_min.xyz, S.root_max.xyz, o.xyz, d.xyz, rinv), kTmin))
+      cur = S.root_leaf >= 0 ? ~S.root_leaf : 0;
+    else
+      cur = kDone;
+  };
+  begin_segment();
+
+  for (;;) {
+    // ---- T: one node step (objdef.h:252-273 with child boxes)
+    const bool in_t = live && cur >= 0;
+    if (__ballot(in_t)) {
+      if (STATS && lane == __builtin_ctzll(__ballot(1))) w_t++;
+      if (in_t) {
+        const DevNode N = S.nodes[cur];
+        if (STATS) n_nodes++;
+        f3 lmin = N.a.xyz, lmax = (f3){N.a.w, N.b.x, N.b.y};
+        f3 rmin = (f3){N.b.z, N.b.w, N.c.x}, rmax = N.c.yzw;
+        BoxT bl = box_test<LIT>(lmin, lmax, o.xyz, d.xyz, rinv);
+        BoxT br = box_test<LIT>(rmin, rmax, o.xyz, d.xyz, rinv);
+        bool hl = slab_pass(bl, kTmin), hr = slab_pass(br, kTmin);
+        if (PRUNE) {
+          const float lim = best_t + S.prune_margin;
+          hl = hl && !(bl.tnear > lim);
+          hr = hr && !(br.tnear > lim);
+        }
+        if (hl && hr) stk[(sp++) * 64] = N.right;  // push right, descend left
+        cur = hl ? N.left : (hr ? N.right : kPop);
+        if (cur == kPop) cur = sp == 0 ? kDone : stk[(--sp) * 64];
+      }
     }
-    bool done;
-    if (tr.t >= kFltMax) {  // shade.cl:92-96 — miss: black, terminate
-      color = (f4){0.0f, 0.0f, 0.0f, 0.0f};
-      done = true;
-    } else {
-      const DevTri &T = A.S.tris[tr.tri];
-      ShadeIn in;
-      in.o = o;
-      in.d = d;
-      in.nrm = (f4){T.nrm.x, T.nrm.y, T.nrm.z, 0.0f};
-      if (cl_dot3(d.xyz, in.nrm.xyz) > 0) in.nrm = -in.nrm;  // intersect.cl:23-25
-      in.pt = o + tr.t * d;                                    // objdef.h:218
-      in.mat = as_i(T.nrm.w);
-      ShadeOut so = shade_hit(A.S.mats, in, color, seed, A.max_depth);
-      if (STATS) n_bad += so.bad;
-      color = so.color;
-      o = so.o;
-      d = so.d;
-      done = (as_i(o.w) & (int32_t)MCPT_TERMINATED) != 0;
+    // ---- L: triangle tests, batched
+    const bool in_l = live && cur < 0 && cur != kDone;
+    const unsigned long long ml = __ballot(in_l);
+    if (ml && (__popcll(ml) >= A.th_leaf || !__ballot(live && cur >= 0))) {
+      if (STATS && lane == __builtin_ctzll(__ballot(1))) w_l++;
+      if (in_l) {
+        const int32_t id = ~cur;
+        const DevTri T = S.tris[id];
+        TriHit h = cramer(d.xyz, T.nab.xyz, T.nac.xyz, T.v0.xyz - o.xyz, T.nrm.xyz, kTmin);
+        if (STATS) n_tests++;
+        if (h.accept && best_t - h.t >= kEps) {  // objdef.h:213 — first-found wins near-ties
+          best_t = h.t;
+          best_tri = id;
+        }
+        cur = sp == 0 ? kDone : stk[(--sp) * 64];
+      }
     }
-    if (done) {
-      // ColorOut: history runs while attemptCount <= MAX_ATTEMPT (colorout.cpp:56)
-      if (A.frame_begin + f <= A.max_attempt) (void)accumulate_one(color, hist, cnt, A.max_attempt);
-      ++f;
-      o = o0;  // no jitter: every frame re-shoots the same primary ray
-      d = d0;
-      color = (f4){1.0f, 1.0f, 1.0f, 1.0f};
+    // ---- S: finish the segment (shade.cl), accumulate (history.cl), next segment
+    const bool in_s = live && cur == kDone;
+    const unsigned long long ms = __ballot(in_s);
+    if (ms && (__popcll(ms) >= A.th_shade || !__ballot(live && cur != kDone))) {
+      if (STATS && lane == __builtin_ctzll(__ballot(1))) w_s++;
+      if (in_s) {
+        if (STATS) n_seg++;
+        bool done;
+        if (best_t >= kFltMax) {  // shade.cl:92-96 — miss: black, terminate
+          color = (f4){0.0f, 0.0f, 0.0f, 0.0f};
+          done = true;
+        } else {
+          const f4 tn = S.tris[best_tri].nrm;
+          ShadeIn in;
+          in.o = o;
+          in.d = d;
+          in.nrm = (f4){tn.x, tn.y, tn.z, 0.0f};
+          if (cl_dot3(d.xyz, in.nrm.xyz) > 0) in.nrm = -in.nrm;  // intersect.cl:23-25
+          in.pt = o + best_t * d;                                  // objdef.h:218
+          in.mat = as_i(tn.w);
+          ShadeOut so = shade_hit(S.mats, in, color, seed, A.max_depth);
+          if (STATS) n_bad += so.bad;
+          color = so.color;
+          o = so.o;
+          d = so.d;
+          done = (as_i(o.w) & (int32_t)MCPT_TERMINATED) != 0;
+        }
+        if (done) {
+          // ColorOut: history runs while attemptCount <= MAX_ATTEMPT (colorout.cpp:56)
+          if (A.frame_begin + f <= A.max_attempt) (void)accumulate_one(color, hist, cnt, A.max_attempt);
+          ++f;
+          live = f < A.frames;
+          o = o0;  // no jitter: every frame re-shoots the same primary ray
+          d = d0;
+          color = (f4){1.0f, 1.0f, 1.0f, 1.0f};
+        }
+        if (live) begin_segment();
+      }
     }
+    if (!__ballot(live)) break;
   }
   A.seeds[pid] = seed;
   A.hist[pid] = hist;
@@ -408,6 +487,11 @@ __global__ void __launch_bounds__(64) k_render(RenderArgs A) {
     atomicAdd(&A.stats[1], n_nodes);
     atomicAdd(&A.stats[2], n_tests);
     if (n_bad) atomicAdd(&A.stats[3], n_bad);
+    if (w_t | w_l | w_s) {
+      atomicAdd(&A.stats[4], w_t);
+      atomicAdd(&A.stats[5], w_l);
+      atomicAdd(&A.stats[6], w_s);
+    }
   }
 }
 
@@ -518,7 +602,7 @@ int mcpt_ctx_create(int32_t device, mcpt_ctx **out) {
   mcpt_ctx *c = new mcpt_ctx();
   c->device = device;
   std::memset(&c->last, 0, sizeof(c->last));
-  if (hipMalloc(&c->d_stats, 4 * sizeof(unsigned long long)) != hipSuccess ||
+  if (hipMalloc(&c->d_stats, 8 * sizeof(unsigned long long)) != hipSuccess ||
       hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess) {
     delete c;
     return mcpt::fail(MCPT_ERR_HIP, "ctx_create: allocation failed");
@@ -688,6 +772,12 @@ int mcpt_render_frames(mcpt_ctx *ctx, const mcpt_scene *scene, const mcpt_camera
   A.max_depth = p->max_depth;
   A.max_attempt = p->max_attempt;
   A.stack_depth = scene->stack_depth;
+  A.th_leaf = 8;
+  A.th_shade = 16;
+  if (const char *e = std::getenv("MCPT_PHASE_THRESHOLDS")) {  // tuning knob: "leaf,shade"
+    int a = 0, b = 0;
+    if (std::sscanf(e, "%d,%d", &a, &b) == 2 && a >= 1 && b >= 1) A.th_leaf = a, A.th_shade = b;
+  }
   const int64_t tiles = (int64_t)A.tiles_x * ((A.local_rows + 7) / 8);
   const size_t lds = (size_t)scene->stack_depth * 64 * sizeof(int32_t);
   int fpl = p->frames_per_launch;
@@ -695,7 +785,7 @@ int mcpt_render_frames(mcpt_ctx *ctx, const mcpt_scene *scene, const mcpt_camera
     int64_t px = (int64_t)p->width * A.local_rows;
     fpl = (int)std::max<int64_t>(1, std::min<int64_t>(p->frames, (int64_t(1) << 26) / std::max<int64_t>(px, 1)));
   }
-  if (ctx->stats_on) HIP_OK(hipMemsetAsync(ctx->d_stats, 0, 4 * sizeof(unsigned long long), st));
+  if (ctx->stats_on) HIP_OK(hipMemsetAsync(ctx->d_stats, 0, 8 * sizeof(unsigned long long), st));
   HIP_OK(hipEventRecord(ctx->ev0, st));
   int launches = 0;
   if (tiles > 0 && p->frames > 0) {
@@ -725,12 +815,15 @@ int mcpt_render_frames(mcpt_ctx *ctx, const mcpt_scene *scene, const mcpt_camera
   ctx->last.kernel_ms = ms;
   ctx->last.launches = launches;
   if (ctx->stats_on) {
-    unsigned long long h[4];
+    unsigned long long h[8];
     HIP_OK(hipMemcpy(h, ctx->d_stats, sizeof(h), hipMemcpyDeviceToHost));
     ctx->last.segments = h[0];
     ctx->last.node_visits = h[1];
     ctx->last.tri_tests = h[2];
     ctx->last.bad_material = h[3];
+    ctx->last.wave_node_phases = h[4];
+    ctx->last.wave_leaf_phases = h[5];
+    ctx->last.wave_shade_phases = h[6];
   }
   return MCPT_OK;
 }

@@ -42,6 +42,11 @@ def main():
                 print("   segments %.3g (%.2f/path) nodes/seg %.2f tris/seg %.2f bad %d active Mseg/s %.1f" % (
                     seg, seg / (w * h * frames), s["node_visits"] / seg, s["tri_tests"] / seg, s["bad_material"],
                     seg / dt / 1e6))
+                if s["wave_node_phases"]:
+                    print("   SIMT: node %.3f leaf %.3f shade %.3f (lanes active per phase / 64)" % (
+                        s["node_visits"] / (64.0 * s["wave_node_phases"]),
+                        s["tri_tests"] / (64.0 * max(s["wave_leaf_phases"], 1)),
+                        seg / (64.0 * max(s["wave_shade_phases"], 1))))
 
 
 if __name__ == "__main__":
