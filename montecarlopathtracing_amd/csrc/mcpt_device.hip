@@ -51,12 +51,13 @@ struct __attribute__((aligned(16))) DevNode {
   int32_t left, right, pad0, pad1;  // >= 0 internal node, < 0 leaf: ~triangle
 };
 // Cramer-ready triangle: v0, -(v1-v0), -(v2-v0) exactly as objdef.h:190-199
-// forms them, plus the packed normal (.w = material id bits).
+// forms them, plus the packed normal (.w = material id bits).  The .w lanes
+// of v0/nab/nac carry the three triangle-only minors of cramer_reduced.
 struct __attribute__((aligned(16))) DevTri {
-  f4 v0;
-  f4 nab;
-  f4 nac;
-  f4 nrm;
+  f4 v0;   // .w = m_x1
+  f4 nab;  // .w = m_y4
+  f4 nac;  // .w = m_y8
+  f4 nrm;  // .w = material id bits
 };
 static_assert(sizeof(DevNode) == 64 && sizeof(DevTri) == 64, "64-B records");
 
@@ -85,6 +86,9 @@ struct mcpt_ctx {
   int device;
   bool stats_on = false;
   unsigned long long *d_stats = nullptr;  // segments, nodes, tris, bad, wave T/L/S phases
+  int32_t *d_queue = nullptr;             // k_render work-queue heads, one per launch
+  int32_t queue_cap = 0;
+  int32_t resident_blocks[2] = {0, 0};   // occupancy of k_render<EXACT|NOPRUNE> (64-thread blocks/CU)
   mcpt_stats last;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
 };
@@ -116,10 +120,13 @@ __device__ inline BoxT box_test(f3 bmin, f3 bmax, f3 o, f3 d, f3 rinv) {
   return slab(bmin, bmax, o, rinv);
 }
 
+template <bool LITERAL>
 __device__ inline void test_tri(const DevTri *__restrict__ tris, int32_t id, f3 o, f3 d, float tmin,
                                 Trace &tr) {
   const DevTri T = tris[id];
-  TriHit h = cramer(d, T.nab.xyz, T.nac.xyz, T.v0.xyz - o, T.nrm.xyz, tmin);
+  TriHit h = LITERAL ? cramer(d, T.nab.xyz, T.nac.xyz, T.v0.xyz - o, T.nrm.xyz, tmin)
+                     : cramer_reduced(d, T.nab.xyz, T.nac.xyz, T.v0.xyz - o, T.nrm.xyz, T.v0.w, T.nab.w,
+                                      T.nac.w, tmin);
   tr.tests++;
   if (h.accept) {
     tr.last = id;
@@ -181,7 +188,7 @@ __device__ inline Trace traverse(const SceneView &S, f3 o, f3 d, float tmin, int
     }
     // ---- all lanes: test the pending leaf, then continue from the stack
     if (cur != kDone) {
-      test_tri(S.tris, ~cur, o, d, tmin, tr);
+      test_tri<LITERAL>(S.tris, ~cur, o, d, tmin, tr);
       cur = sp == 0 ? kDone : stk[(--sp) * stride];
     }
   }
@@ -189,12 +196,23 @@ __device__ inline Trace traverse(const SceneView &S, f3 o, f3 d, float tmin, int
 }
 
 // --------------------------------------------------------------- generateRay
-__device__ inline void gen_ray(const mcpt_camera &cam, uint32_t idx, uint32_t idy, uint32_t w, uint32_t h,
-                               f4 &o, f4 &dir) {
-  // rayGenerator.cl:1-31 (NDRange {W, H}: width/height are size_t there)
+// rayGenerator.cl:1-31.  The per-launch constants (0.5/tan(arg/2) and W/H,
+// identical in every work-item of the reference) are split off so the fused
+// kernel can keep them in scalar registers; the arithmetic is unchanged.
+struct CamConst {
+  float distance, ratio;
+};
+__device__ inline CamConst cam_const(const mcpt_camera &cam, uint32_t w, uint32_t h) {
+  size_t width = w, height = h;  // NDRange {W, H}: get_global_size is a size_t
+  CamConst c;
+  c.ratio = width * 1.0f / height;
+  c.distance = 0.5f / cl_tan(cam.arg / 2);
+  return c;
+}
+__device__ inline void gen_ray_px(const mcpt_camera &cam, CamConst cc, uint32_t idx, uint32_t idy, uint32_t w,
+                                  uint32_t h, f4 &o, f4 &dir) {
   size_t width = w, height = h;
   float px = ((float)idx) / width, py = (float)idy / height;
-  float ratio = width * 1.0f / height;
   const f4 cdir = (f4){cam.direction[0], cam.direction[1], cam.direction[2], cam.direction[3]};
   const f4 chor = (f4){cam.horizontal[0], cam.horizontal[1], cam.horizontal[2], cam.horizontal[3]};
   const f4 cup = (f4){cam.up[0], cam.up[1], cam.up[2], cam.up[3]};
@@ -202,16 +220,21 @@ __device__ inline void gen_ray(const mcpt_camera &cam, uint32_t idx, uint32_t id
   if (cam.camera_type == 0) {
     float temp1 = px - 0.5f;
     float temp2 = py - 0.5f;
-    float distance = 0.5f / cl_tan(cam.arg / 2);
+    float distance = cc.distance, ratio = cc.ratio;
     f4 dd = cdir * distance + temp1 * chor * ratio + temp2 * cup;
     o = ccen;
     dir = cl_normalize(dd);
   } else {
+    float ratio = cc.ratio;
     o = ccen + (px - 0.5f) * (cam.arg) * (chor)*ratio + (py - 0.5f) * (cam.arg) * (cup);
     dir = cl_normalize(cdir);
   }
   o.w = as_f(0);
   dir.w = as_f((int32_t)(idy * w + idx));
+}
+__device__ inline void gen_ray(const mcpt_camera &cam, uint32_t idx, uint32_t idy, uint32_t w, uint32_t h,
+                               f4 &o, f4 &dir) {
+  gen_ray_px(cam, cam_const(cam, w, h), idx, idy, w, h, o, dir);
 }
 
 // -------------------------------------------------------------------- shade
@@ -335,6 +358,7 @@ struct RenderArgs {
   int32_t max_depth, max_attempt, frame_begin, frames;
   int32_t stack_depth;
   int32_t th_leaf, th_shade;  // lanes waiting before the L / S phase runs
+  int32_t *queue;             // pixel work-queue head (zeroed before each launch)
 };
 
 __device__ inline int32_t global_row(int32_t lr, const RenderArgs &A) {
@@ -344,14 +368,23 @@ __device__ inline int32_t global_row(int32_t lr, const RenderArgs &A) {
 
 constexpr float kTmin = 0.001f;  // host EPSILON passed as tmin (oclbasic.h:193, scenebuild.cpp:125)
 
-// The fused kernel is a per-wave state machine.  Every lane is in one of
+// The fused kernel is a persistent per-wave state machine.
+//
+// Work queue: a launch renders `frames` frames of every pixel of this GPU's
+// stripes.  Pixels are handed out in 8x8-tile order by one atomic counter;
+// a lane owns a pixel for all of its frames (the seed chain and the running
+// mean are sequential per pixel), writes the pixel back when done and pulls
+// the next one, so lanes whose paths were short keep working instead of
+// idling until the wave's slowest pixel finishes.
+//
+// Phases.  Every lane with a pixel is in one of
 //   T: walking internal BVH nodes (cur >= 0)
 //   L: holding a leaf whose triangle must be tested (cur = ~tri)
 //   S: segment traced (cur == kDone): shade, accumulate, start the next segment
 // and each loop iteration runs one T step for the T lanes, then the L phase
-// and the S phase only when enough lanes are waiting for them (or nothing
-// else can run).  Expensive phases therefore execute with most of the wave
-// active instead of once per diverging lane.  Each lane's own
+// and the S phase only when enough lanes wait for them (or nothing else can
+// run).  Expensive phases therefore execute with most of the wave active
+// instead of once per diverging lane.  Each lane's own
 // sequence of operations is exactly the reference's, so results are unchanged.
 template <int MODE, bool STATS>
 __global__ void __launch_bounds__(64, MCPT_WAVES_PER_SIMD) k_render(RenderArgs A) {
@@ -360,30 +393,29 @@ __global__ void __launch_bounds__(64, MCPT_WAVES_PER_SIMD) k_render(RenderArgs A
   extern __shared__ int32_t lds_stack[];
   const int lane = threadIdx.x;
   int32_t *stk = lds_stack + lane;  // column-major [depth][64]: conflict-free
-  const int32_t tile = blockIdx.x;
-  const int32_t x = (tile % A.tiles_x) * 8 + (lane & 7);
-  const int32_t lr = (tile / A.tiles_x) * 8 + (lane >> 3);
-  if (x >= A.W || lr >= A.local_rows) return;
-  const int32_t y = global_row(lr, A);
-  if (y >= A.H) return;
-  const int32_t pid = y * A.W + x;
   const SceneView &S = A.S;
-
-  uint32_t seed = A.seeds[pid];
-  f4 hist = A.hist[pid];
-  int32_t cnt = A.count[pid];
-  f4 o0, d0;
-  gen_ray(A.cam, (uint32_t)x, (uint32_t)y, (uint32_t)A.W, (uint32_t)A.H, o0, d0);
 
   unsigned long long n_seg = 0, n_nodes = 0, n_tests = 0, n_bad = 0;
   unsigned long long w_t = 0, w_l = 0, w_s = 0;
-  int32_t f = 0;
-  bool live = A.frames > 0;
-  f4 o = o0, d = d0;
-  f4 color = (f4){1.0f, 1.0f, 1.0f, 1.0f};
-  f3 rinv;
-  float best_t;
-  int32_t best_tri, cur, sp;
+  // pixel state
+  bool alive = true;   // queue not exhausted for this lane
+  bool has_px = false; // owns a pixel
+  int32_t pid = 0, f = 0, cnt = 0;
+  uint32_t seed = 0, pxy = 0;  // pxy = x | y << 16
+  f4 hist = (f4){0.0f, 0.0f, 0.0f, 0.0f};
+  f4 o = hist, d = hist, color = hist;
+  // uniform generateRay constants, moved to scalar registers
+  CamConst cc = cam_const(A.cam, (uint32_t)A.W, (uint32_t)A.H);
+  cc.distance = as_f(__builtin_amdgcn_readfirstlane(as_i(cc.distance)));
+  cc.ratio = as_f(__builtin_amdgcn_readfirstlane(as_i(cc.ratio)));
+  auto primary = [&]() {  // no jitter: every frame re-shoots the same primary ray
+    gen_ray_px(A.cam, cc, pxy & 0xFFFFu, pxy >> 16, (uint32_t)A.W, (uint32_t)A.H, o, d);
+    color = (f4){1.0f, 1.0f, 1.0f, 1.0f};
+  };
+  // path / traversal state (declared with the pixel state below)
+  f3 rinv = (f3){0.0f, 0.0f, 0.0f};
+  float best_t = kFltMax;
+  int32_t best_tri = -1, cur = kDone, sp = 0;
   auto begin_segment = [&]() {
     rinv.x = __builtin_amdgcn_rcpf(d.x);
     rinv.y = __builtin_amdgcn_rcpf(d.y);
@@ -396,9 +428,45 @@ __global__ void __launch_bounds__(64, MCPT_WAVES_PER_SIMD) k_render(RenderArgs A
     else
       cur = kDone;
   };
-  begin_segment();
+  const int32_t n_items = A.tiles_x * ((A.local_rows + 7) >> 3) * 64;
 
   for (;;) {
+    // ---- fetch: lanes without a pixel take the next queue entries (one atomic per wave)
+    {
+      const bool need = alive && !has_px;
+      const unsigned long long mn = __ballot(need);
+      if (mn) {
+        const int leader = __builtin_ctzll(mn);
+        int32_t base = 0;
+        if (lane == leader) base = atomicAdd(A.queue, __popcll(mn));
+        base = __shfl(base, leader);
+        if (need) {
+          const int32_t q = base + (int32_t)__builtin_amdgcn_mbcnt_hi((uint32_t)(mn >> 32),
+                                                                       __builtin_amdgcn_mbcnt_lo((uint32_t)mn, 0));
+          if (q >= n_items) {
+            alive = false;
+          } else {
+            const int32_t tile = q >> 6, k = q & 63;
+            const int32_t x = (tile % A.tiles_x) * 8 + (k & 7);
+            const int32_t lr = (tile / A.tiles_x) * 8 + (k >> 3);
+            const int32_t y = lr < A.local_rows ? global_row(lr, A) : A.H;
+            if (x < A.W && y < A.H) {  // else: an edge-tile hole, fetch again
+              has_px = true;
+              pid = y * A.W + x;
+              seed = A.seeds[pid];
+              hist = A.hist[pid];
+              cnt = A.count[pid];
+              f = 0;
+              pxy = (uint32_t)x | ((uint32_t)y << 16);
+              primary();
+              begin_segment();
+            }
+          }
+        }
+      }
+    }
+    if (!__ballot(alive)) break;
+    const bool live = has_px;
     // ---- T: one node step (objdef.h:252-273 with child boxes)
     const bool in_t = live && cur >= 0;
     if (__ballot(in_t)) {
@@ -429,7 +497,9 @@ __global__ void __launch_bounds__(64, MCPT_WAVES_PER_SIMD) k_render(RenderArgs A
       if (in_l) {
         const int32_t id = ~cur;
         const DevTri T = S.tris[id];
-        TriHit h = cramer(d.xyz, T.nab.xyz, T.nac.xyz, T.v0.xyz - o.xyz, T.nrm.xyz, kTmin);
+        TriHit h = LIT ? cramer(d.xyz, T.nab.xyz, T.nac.xyz, T.v0.xyz - o.xyz, T.nrm.xyz, kTmin)
+                       : cramer_reduced(d.xyz, T.nab.xyz, T.nac.xyz, T.v0.xyz - o.xyz, T.nrm.xyz, T.v0.w,
+                                        T.nab.w, T.nac.w, kTmin);
         if (STATS) n_tests++;
         if (h.accept && best_t - h.t >= kEps) {  // objdef.h:213 — first-found wins near-ties
           best_t = h.t;
@@ -469,19 +539,18 @@ __global__ void __launch_bounds__(64, MCPT_WAVES_PER_SIMD) k_render(RenderArgs A
           // ColorOut: history runs while attemptCount <= MAX_ATTEMPT (colorout.cpp:56)
           if (A.frame_begin + f <= A.max_attempt) (void)accumulate_one(color, hist, cnt, A.max_attempt);
           ++f;
-          live = f < A.frames;
-          o = o0;  // no jitter: every frame re-shoots the same primary ray
-          d = d0;
-          color = (f4){1.0f, 1.0f, 1.0f, 1.0f};
+          if (f < A.frames) primary();
+          if (f == A.frames) {  // pixel complete: write back, fetch another next iteration
+            A.seeds[pid] = seed;
+            A.hist[pid] = hist;
+            A.count[pid] = cnt;
+            has_px = false;
+          }
         }
-        if (live) begin_segment();
+        if (has_px) begin_segment();
       }
     }
-    if (!__ballot(live)) break;
   }
-  A.seeds[pid] = seed;
-  A.hist[pid] = hist;
-  A.count[pid] = cnt;
   if (STATS) {
     atomicAdd(&A.stats[0], n_seg);
     atomicAdd(&A.stats[1], n_nodes);
@@ -615,6 +684,7 @@ int mcpt_ctx_destroy(mcpt_ctx *c) {
   if (!c) return MCPT_OK;
   (void)hipSetDevice(c->device);
   if (c->d_stats) (void)hipFree(c->d_stats);
+  if (c->d_queue) (void)hipFree(c->d_queue);
   if (c->ev0) (void)hipEventDestroy(c->ev0);
   if (c->ev1) (void)hipEventDestroy(c->ev1);
   delete c;
@@ -657,6 +727,10 @@ int mcpt_scene_upload(mcpt_ctx *ctx, const mcpt_triangle *tris, int64_t n_tris, 
     int32_t m;
     std::memcpy(&m, &tris[i].normal[3], 4);
     if (m < 0 || m >= n_mats) return mcpt::fail(MCPT_ERR_ARG, "scene_upload: triangle material id out of range");
+    for (int k = 0; k < 3; ++k)
+      for (int j = 0; j < 3; ++j)
+        if (!std::isfinite(tris[i].v[k][j]))
+          return mcpt::fail(MCPT_ERR_ARG, "scene_upload: non-finite vertex coordinate");
   }
   // reference node index -> device index: internal nodes keep their index in
   // a compacted array (the HLBVH puts them at [0, n-2]); leaves become ~tri.
@@ -683,9 +757,12 @@ int mcpt_scene_upload(mcpt_ctx *ctx, const mcpt_triangle *tris, int64_t n_tris, 
     const mcpt_triangle &t = tris[i];
     DevTri &d = dt[i];
     // objdef.h:190-199: AB = (v1 - v0).s012, AC = (v2 - v0).s012, matrix rows -AB, -AC
-    d.v0 = (f4){t.v[0][0], t.v[0][1], t.v[0][2], 0.0f};
-    d.nab = (f4){-(t.v[1][0] - t.v[0][0]), -(t.v[1][1] - t.v[0][1]), -(t.v[1][2] - t.v[0][2]), 0.0f};
-    d.nac = (f4){-(t.v[2][0] - t.v[0][0]), -(t.v[2][1] - t.v[0][1]), -(t.v[2][2] - t.v[0][2]), 0.0f};
+    const float b1 = -(t.v[1][0] - t.v[0][0]), b2 = -(t.v[1][1] - t.v[0][1]), b3 = -(t.v[1][2] - t.v[0][2]);
+    const float c1 = -(t.v[2][0] - t.v[0][0]), c2 = -(t.v[2][1] - t.v[0][1]), c3 = -(t.v[2][2] - t.v[0][2]);
+    // triangle-only minors of cramer_reduced (std::fma = the device's fused v_fma_f32)
+    d.v0 = (f4){t.v[0][0], t.v[0][1], t.v[0][2], std::fma(b2, c3, -(c2 * b3))};
+    d.nab = (f4){b1, b2, b3, std::fma(b1, c3, -(c1 * b3))};
+    d.nac = (f4){c1, c2, c3, std::fma(b1, c2, -(c1 * b2))};
     d.nrm = (f4){t.normal[0], t.normal[1], t.normal[2], t.normal[3]};
   }
   // pruning margin: 2^-10 of the scene diagonal
@@ -738,7 +815,8 @@ int mcpt_scene_destroy(mcpt_scene *s) {
 static int check_render(const mcpt_render_params *p) {
   if (p->width <= 0 || p->height <= 0 || p->max_depth <= 0 || p->max_depth > 0xFFFF || p->frames < 0 ||
       p->frame_begin < 0 || p->stripe_count <= 0 || p->stripe_rows <= 0 || p->stripe_index < 0 ||
-      p->stripe_index >= p->stripe_count || (int64_t)p->width * p->height > (int64_t)INT32_MAX)
+      p->stripe_index >= p->stripe_count || p->width > 65535 || p->height > 65535 ||
+      (int64_t)p->width * p->height > (int64_t)INT32_MAX)
     return mcpt::fail(MCPT_ERR_ARG, "render: bad parameters");
   if (p->mode != MCPT_MODE_EXACT && p->mode != MCPT_MODE_NOPRUNE) return mcpt::fail(MCPT_ERR_ARG, "render: bad mode");
   return MCPT_OK;
@@ -785,23 +863,43 @@ int mcpt_render_frames(mcpt_ctx *ctx, const mcpt_scene *scene, const mcpt_camera
     int64_t px = (int64_t)p->width * A.local_rows;
     fpl = (int)std::max<int64_t>(1, std::min<int64_t>(p->frames, (int64_t(1) << 26) / std::max<int64_t>(px, 1)));
   }
+  const int n_launch = (p->frames + fpl - 1) / fpl;
+  if (n_launch > ctx->queue_cap) {  // one queue head per launch, zeroed by a single memset
+    if (ctx->d_queue) HIP_OK(hipFree(ctx->d_queue));
+    ctx->d_queue = nullptr;
+    ctx->queue_cap = 0;
+    HIP_OK(hipMalloc(&ctx->d_queue, (size_t)std::max(n_launch, 64) * sizeof(int32_t)));
+    ctx->queue_cap = std::max(n_launch, 64);
+  }
+  // persistent grid: as many 64-lane workgroups as can be resident at once
+  const bool noprune = p->mode == MCPT_MODE_NOPRUNE;
+  const void *kfn = noprune ? (ctx->stats_on ? (const void *)k_render<MCPT_MODE_NOPRUNE, true>
+                                             : (const void *)k_render<MCPT_MODE_NOPRUNE, false>)
+                            : (ctx->stats_on ? (const void *)k_render<MCPT_MODE_EXACT, true>
+                                             : (const void *)k_render<MCPT_MODE_EXACT, false>);
+  int per_cu = 0, n_cu = 0;
+  HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kfn, 64, lds));
+  HIP_OK(hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, ctx->device));
+  const int64_t grid = std::max<int64_t>(1, std::min<int64_t>(tiles, (int64_t)std::max(per_cu, 1) * n_cu));
   if (ctx->stats_on) HIP_OK(hipMemsetAsync(ctx->d_stats, 0, 8 * sizeof(unsigned long long), st));
   HIP_OK(hipEventRecord(ctx->ev0, st));
   int launches = 0;
   if (tiles > 0 && p->frames > 0) {
+    HIP_OK(hipMemsetAsync(ctx->d_queue, 0, (size_t)n_launch * sizeof(int32_t), st));
     for (int f0 = 0; f0 < p->frames; f0 += fpl) {
       A.frame_begin = p->frame_begin + f0;
       A.frames = std::min(fpl, p->frames - f0);
-      if (p->mode == MCPT_MODE_NOPRUNE) {
+      A.queue = ctx->d_queue + launches;
+      if (noprune) {
         if (ctx->stats_on)
-          hipLaunchKernelGGL((k_render<MCPT_MODE_NOPRUNE, true>), dim3(tiles), dim3(64), lds, st, A);
+          hipLaunchKernelGGL((k_render<MCPT_MODE_NOPRUNE, true>), dim3(grid), dim3(64), lds, st, A);
         else
-          hipLaunchKernelGGL((k_render<MCPT_MODE_NOPRUNE, false>), dim3(tiles), dim3(64), lds, st, A);
+          hipLaunchKernelGGL((k_render<MCPT_MODE_NOPRUNE, false>), dim3(grid), dim3(64), lds, st, A);
       } else {
         if (ctx->stats_on)
-          hipLaunchKernelGGL((k_render<MCPT_MODE_EXACT, true>), dim3(tiles), dim3(64), lds, st, A);
+          hipLaunchKernelGGL((k_render<MCPT_MODE_EXACT, true>), dim3(grid), dim3(64), lds, st, A);
         else
-          hipLaunchKernelGGL((k_render<MCPT_MODE_EXACT, false>), dim3(tiles), dim3(64), lds, st, A);
+          hipLaunchKernelGGL((k_render<MCPT_MODE_EXACT, false>), dim3(grid), dim3(64), lds, st, A);
       }
       HIP_OK(hipGetLastError());
       ++launches;

@@ -192,6 +192,56 @@ __device__ inline TriHit cramer(f3 rd, f3 nab, f3 nac, f3 aro, f3 realn, float t
   return r;
 }
 
+// The same test with the reference matrix's constant entries eliminated.
+// Row a = (rd, 0), b = (-(v1-v0), 0), c = (-(v2-v0), 0), d = (0, 0, 0, 1):
+// every minor above then reduces to ONE contracted 2x2 term, e.g.
+//   m3(b2,b3,0, c2,c3,0, 0,0,1) = fma(0, +-0, fma(b2, m2(c3,0,0,1), -(c2*m2(b3,0,0,1))))
+//                              = fma(b2, c3, -(c2*b3))            (exactly)
+// because x*1 = x, y + (+-0) = y and x*0 = +-0 for finite x (vertices are
+// checked finite at upload); only the sign of an exactly-zero intermediate can
+// differ, and a zero b/c/t/det compares identically with either sign.  The
+// three triangle-only minors come precomputed (same fma, on the host):
+//   m_x1 = fma(b2,c3,-(c2*b3)), m_y4 = fma(b1,c3,-(c1*b3)), m_y8 = fma(b1,c2,-(c1*b2)).
+// The nine quotients use x * rcp(det) for the reference's 2.5-ulp x / det
+// (= ldexp(mant(x)*rcp(mant(det)), ex-edet)): identical whenever the quotient
+// is a normal float, i.e. unless a cofactor quotient falls below 2^-126.
+__device__ inline TriHit cramer_reduced(f3 rd, f3 nab, f3 nac, f3 aro, f3 realn, float m_x1, float m_y4,
+                                        float m_y8, float tmin) {
+  TriHit r;
+  r.accept = false;
+  r.t = 0.0f;
+  if (__builtin_fabsf(cl_dot3(realn, rd)) < kEps) return r;
+  const float a1 = rd.x, a2 = rd.y, a3 = rd.z;
+  const float b1 = nab.x, b2 = nab.y, b3 = nab.z;
+  const float c1 = nac.x, c2 = nac.y, c3 = nac.z;
+  const float x2 = __builtin_fmaf(a2, c3, -(c2 * a3));
+  const float x3 = __builtin_fmaf(a2, b3, -(b2 * a3));
+  const float det = __builtin_fmaf(c1, x3, __builtin_fmaf(a1, m_x1, -(b1 * x2)));
+  if (__builtin_fabsf(det) < kEps) return r;
+  const float rdet = __builtin_amdgcn_rcpf(det);
+  // b = dot(A_Ro, (s1, s5, s9))
+  const float s1 = -x2 * rdet;
+  const float s5 = __builtin_fmaf(a1, c3, -(c1 * a3)) * rdet;
+  const float s9 = -__builtin_fmaf(a1, c2, -(c1 * a2)) * rdet;
+  const float bb = cl_dot3(aro, (f3){s1, s5, s9});
+  if (bb < 0) return r;
+  // c = dot(A_Ro, (s2, s6, s10))
+  const float s2 = x3 * rdet;
+  const float s6 = -__builtin_fmaf(a1, b3, -(b1 * a3)) * rdet;
+  const float sa = __builtin_fmaf(a1, b2, -(b1 * a2)) * rdet;
+  const float cc = cl_dot3(aro, (f3){s2, s6, sa});
+  if (cc < 0 || bb + cc > 1) return r;
+  const float s0 = m_x1 * rdet;
+  if (s0 == kFltMax) return r;
+  const float s4 = -m_y4 * rdet;
+  const float s8 = m_y8 * rdet;
+  const float t = cl_dot3(aro, (f3){s0, s4, s8});
+  if (t <= tmin) return r;
+  r.t = t;
+  r.accept = true;
+  return r;
+}
+
 // intersectAABB (objdef.h:223-237).  (bb - o) / d under the 2.5-ulp OpenCL
 // division is ldexp(mant(x) * rcp(mant(d)), ex - ed) == x * rcp(d) for every
 // normal-range quotient; rcp(d) is hoisted per ray (verified on the GPU
