@@ -45,9 +45,9 @@ int fail(int code, const std::string &msg);  // mcpt_host.cpp
 // BOTH children's boxes so one 64-B fetch decides where to go next
 // (objdef.h:252-273 fetches and tests one 64-B node per step).
 struct __attribute__((aligned(16))) DevNode {
-  f4 a;  // Lmin.x Lmin.y Lmin.z Lmax.x
-  f4 b;  // Lmax.y Lmax.z Rmin.x Rmin.y
-  f4 c;  // Rmin.z Rmax.x Rmax.y Rmax.z
+  f4 a;  // Lmin.x Lmax.x Lmin.y Lmax.y      (min,max) pairs per axis, so the
+  f4 b;  // Lmin.z Lmax.z Rmin.x Rmax.x      slab arithmetic runs on packed
+  f4 c;  // Rmin.y Rmax.y Rmin.z Rmax.z      v_pk_add/v_pk_mul_f32
   int32_t left, right, pad0, pad1;  // >= 0 internal node, < 0 leaf: ~triangle
 };
 // Cramer-ready triangle: v0, -(v1-v0), -(v2-v0) exactly as objdef.h:190-199
@@ -61,7 +61,25 @@ struct __attribute__((aligned(16))) DevTri {
 };
 static_assert(sizeof(DevNode) == 64 && sizeof(DevTri) == 64, "64-B records");
 
+// 4-wide node of the EXACT path: the binary HLBVH with every other level
+// collapsed.  Slots are the node's grandchildren (or a child that is a leaf)
+// in left-to-right order, so visiting passing slots in slot order IS the
+// reference's left-first DFS.  Skipping the middle box test is exact: a
+// grandchild box lies inside its parent's, and (bb - o) * rcp(d) is monotone
+// in bb, so a grandchild's slab interval lies inside its parent's — it can
+// only pass if the parent passes.
+struct __attribute__((aligned(16))) DevNode4 {
+  f4 q[6];          // per slot k: (minx,maxx) (miny,maxy) (minz,maxz) pairs, packed 6 floats/slot
+  int32_t link[4];  // >= 0 internal DevNode4, < 0 leaf ~triangle, kEmptySlot unused
+  f4 pad;
+};
+static_assert(sizeof(DevNode4) == 128, "128-B 4-wide node");
+constexpr int32_t kDone = INT32_MIN;           // traversal finished
+constexpr int32_t kPop = INT32_MIN + 1;        // take the next entry from the stack
+constexpr int32_t kEmptySlot = INT32_MIN + 2;  // unused 4-wide slot
+
 struct SceneView {
+  const DevNode4 *nodes4;
   const DevNode *nodes;
   const DevTri *tris;
   const mcpt_material *mats;
@@ -73,6 +91,8 @@ struct SceneView {
 
 struct mcpt_scene {
   int device;
+  DevNode4 *nodes4 = nullptr;
+  int32_t stack_depth4 = 1;
   DevNode *nodes = nullptr;
   DevTri *tris = nullptr;
   mcpt_material *mats = nullptr;
@@ -120,6 +140,67 @@ __device__ inline BoxT box_test(f3 bmin, f3 bmax, f3 o, f3 d, f3 rinv) {
   return slab(bmin, bmax, o, rinv);
 }
 
+// Both child boxes of a node (objdef.h:223-237 twice).  Packed form: the
+// (min, max) pair of each axis is one float2, so (bb - o) * rcp(d) is one
+// v_pk_add_f32 + one v_pk_mul_f32 per axis and box — the same IEEE operations
+// as the scalar form, two lanes at a time.
+typedef float f2 __attribute__((ext_vector_type(2)));
+__device__ inline BoxT slab_pairs(f2 px, f2 py, f2 pz, f3 o, f3 rinv) {
+  f2 tx = (px - o.x) * rinv.x, ty = (py - o.y) * rinv.y, tz = (pz - o.z) * rinv.z;
+  BoxT r;
+  r.tnear = fmaxf(fmaxf(fminf(tx.x, tx.y), fminf(ty.x, ty.y)), fminf(tz.x, tz.y));
+  r.tfar = fminf(fminf(fmaxf(tx.x, tx.y), fmaxf(ty.x, ty.y)), fmaxf(tz.x, tz.y));
+  return r;
+}
+template <bool LITERAL>
+__device__ inline void child_boxes(const DevNode &N, f3 o, f3 d, f3 rinv, BoxT &bl, BoxT &br) {
+  if (LITERAL) {
+    bl = box_test<true>((f3){N.a.x, N.a.z, N.b.x}, (f3){N.a.y, N.a.w, N.b.y}, o, d, rinv);
+    br = box_test<true>((f3){N.b.z, N.c.x, N.c.z}, (f3){N.b.w, N.c.y, N.c.w}, o, d, rinv);
+  } else {
+    bl = slab_pairs(N.a.xy, N.a.zw, N.b.xy, o, rinv);
+    br = slab_pairs(N.b.zw, N.c.xy, N.c.zw, o, rinv);
+  }
+}
+
+// One 4-wide node: slab test of the 4 slots, then left-first order.
+// Returns the next entry (internal node, leaf, or kPop) and pushes the other
+// passing slots so that they pop in slot order.
+template <bool PRUNE>
+__device__ inline int32_t step4(const DevNode4 &N, f3 o, f3 rinv, float tmin, float lim, int32_t *stk, int &sp,
+                                uint32_t &nodes_ctr) {
+  const f4 q0 = N.q[0], q1 = N.q[1], q2 = N.q[2], q3 = N.q[3], q4 = N.q[4], q5 = N.q[5];
+  BoxT b0 = slab_pairs(q0.xy, q0.zw, q1.xy, o, rinv);
+  BoxT b1 = slab_pairs(q1.zw, q2.xy, q2.zw, o, rinv);
+  BoxT b2 = slab_pairs(q3.xy, q3.zw, q4.xy, o, rinv);
+  BoxT b3 = slab_pairs(q4.zw, q5.xy, q5.zw, o, rinv);
+  const int32_t l0 = N.link[0], l1 = N.link[1], l2 = N.link[2], l3 = N.link[3];
+  bool h0 = slab_pass(b0, tmin) && l0 != kEmptySlot, h1 = slab_pass(b1, tmin) && l1 != kEmptySlot;
+  bool h2 = slab_pass(b2, tmin) && l2 != kEmptySlot, h3 = slab_pass(b3, tmin) && l3 != kEmptySlot;
+  if (PRUNE) {
+    h0 = h0 && !(b0.tnear > lim);
+    h1 = h1 && !(b1.tnear > lim);
+    h2 = h2 && !(b2.tnear > lim);
+    h3 = h3 && !(b3.tnear > lim);
+  }
+  nodes_ctr++;
+  int32_t nxt = kPop;
+  if (h3) nxt = l3;
+  if (h2) {
+    if (nxt != kPop) stk[(sp++) * 64] = nxt;
+    nxt = l2;
+  }
+  if (h1) {
+    if (nxt != kPop) stk[(sp++) * 64] = nxt;
+    nxt = l1;
+  }
+  if (h0) {
+    if (nxt != kPop) stk[(sp++) * 64] = nxt;
+    nxt = l0;
+  }
+  return nxt;
+}
+
 template <bool LITERAL>
 __device__ inline void test_tri(const DevTri *__restrict__ tris, int32_t id, f3 o, f3 d, float tmin,
                                 Trace &tr) {
@@ -145,8 +226,6 @@ __device__ inline void test_tri(const DevTri *__restrict__ tris, int32_t id, f3 
 // nodes until EVERY lane of the wave holds a leaf (or is done); then all lanes
 // with a leaf run the Cramer test together.  Each lane still tests its
 // triangles in exactly the reference's DFS order.
-constexpr int32_t kDone = INT32_MIN;       // traversal finished
-constexpr int32_t kPop = INT32_MIN + 1;    // take the next entry from the stack
 
 template <bool PRUNE, bool LITERAL>
 __device__ inline Trace traverse(const SceneView &S, f3 o, f3 d, float tmin, int32_t *stk, int stride) {
@@ -170,20 +249,22 @@ __device__ inline Trace traverse(const SceneView &S, f3 o, f3 d, float tmin, int
   while (cur != kDone) {
     // ---- walk internal nodes until this lane holds a leaf or is done
     while (cur >= 0) {
-      const DevNode N = nodes[cur];
-      tr.nodes++;
-      f3 lmin = N.a.xyz, lmax = (f3){N.a.w, N.b.x, N.b.y};
-      f3 rmin = (f3){N.b.z, N.b.w, N.c.x}, rmax = N.c.yzw;
-      BoxT bl = box_test<LITERAL>(lmin, lmax, o, d, rinv);
-      BoxT br = box_test<LITERAL>(rmin, rmax, o, d, rinv);
-      bool hl = slab_pass(bl, tmin), hr = slab_pass(br, tmin);
-      if (PRUNE) {
-        const float lim = tr.t + S.prune_margin;
-        hl = hl && !(bl.tnear > lim);
-        hr = hr && !(br.tnear > lim);
+      if (!LITERAL) {  // 4-wide collapsed tree (same DFS order)
+        cur = step4<PRUNE>(S.nodes4[cur], o, rinv, tmin, tr.t + S.prune_margin, stk, sp, tr.nodes);
+      } else {
+        const DevNode N = nodes[cur];
+        tr.nodes++;
+        BoxT bl, br;
+        child_boxes<LITERAL>(N, o, d, rinv, bl, br);
+        bool hl = slab_pass(bl, tmin), hr = slab_pass(br, tmin);
+        if (PRUNE) {
+          const float lim = tr.t + S.prune_margin;
+          hl = hl && !(bl.tnear > lim);
+          hr = hr && !(br.tnear > lim);
+        }
+        if (hl && hr) stk[(sp++) * stride] = N.right;  // reference: push right, descend left
+        cur = hl ? N.left : (hr ? N.right : kPop);
       }
-      if (hl && hr) stk[(sp++) * stride] = N.right;  // reference: push right, descend left
-      cur = hl ? N.left : (hr ? N.right : kPop);
       if (cur == kPop) cur = sp == 0 ? kDone : stk[(--sp) * stride];
     }
     // ---- all lanes: test the pending leaf, then continue from the stack
@@ -336,8 +417,12 @@ __device__ inline ShadeOut shade_hit(const mcpt_material *__restrict__ mats, con
 }
 
 // history.cl:3-28 on one pixel; returns the colour the reference shows.
+// length(now) == 0 is evaluated as "every component is +-0": with IEEE
+// denormals the built-in's rescaling branch makes length() > 0 for any
+// non-zero (or NaN) component, so the two tests agree for every input.
 __device__ inline f4 accumulate_one(f4 now, f4 &hist, int32_t &cnt, int max_attempt) {
-  if (cl_length4(now) == 0 || cnt >= max_attempt) return hist;
+  const bool zero = now.x == 0.0f && now.y == 0.0f && now.z == 0.0f && now.w == 0.0f;
+  if (zero || cnt >= max_attempt) return hist;
   now = (now + hist * cnt) / (cnt + 1);
   hist = now;
   hist.w = 0.0f;
@@ -472,20 +557,24 @@ __global__ void __launch_bounds__(64, MCPT_WAVES_PER_SIMD) k_render(RenderArgs A
     if (__ballot(in_t)) {
       if (STATS && lane == __builtin_ctzll(__ballot(1))) w_t++;
       if (in_t) {
-        const DevNode N = S.nodes[cur];
-        if (STATS) n_nodes++;
-        f3 lmin = N.a.xyz, lmax = (f3){N.a.w, N.b.x, N.b.y};
-        f3 rmin = (f3){N.b.z, N.b.w, N.c.x}, rmax = N.c.yzw;
-        BoxT bl = box_test<LIT>(lmin, lmax, o.xyz, d.xyz, rinv);
-        BoxT br = box_test<LIT>(rmin, rmax, o.xyz, d.xyz, rinv);
-        bool hl = slab_pass(bl, kTmin), hr = slab_pass(br, kTmin);
-        if (PRUNE) {
-          const float lim = best_t + S.prune_margin;
-          hl = hl && !(bl.tnear > lim);
-          hr = hr && !(br.tnear > lim);
+        if (!LIT) {  // 4-wide collapsed tree, same DFS order (DevNode4)
+          uint32_t ctr = 0;
+          cur = step4<PRUNE>(S.nodes4[cur], o.xyz, rinv, kTmin, best_t + S.prune_margin, stk, sp, ctr);
+          if (STATS) n_nodes += ctr;
+        } else {  // NOPRUNE: the reference's binary tree, literal division
+          const DevNode N = S.nodes[cur];
+          if (STATS) n_nodes++;
+          BoxT bl, br;
+          child_boxes<LIT>(N, o.xyz, d.xyz, rinv, bl, br);
+          bool hl = slab_pass(bl, kTmin), hr = slab_pass(br, kTmin);
+          if (PRUNE) {
+            const float lim = best_t + S.prune_margin;
+            hl = hl && !(bl.tnear > lim);
+            hr = hr && !(br.tnear > lim);
+          }
+          if (hl && hr) stk[(sp++) * 64] = N.right;  // push right, descend left
+          cur = hl ? N.left : (hr ? N.right : kPop);
         }
-        if (hl && hr) stk[(sp++) * 64] = N.right;  // push right, descend left
-        cur = hl ? N.left : (hr ? N.right : kPop);
         if (cur == kPop) cur = sp == 0 ? kDone : stk[(--sp) * 64];
       }
     }
@@ -745,13 +834,66 @@ int mcpt_scene_upload(mcpt_ctx *ctx, const mcpt_triangle *tris, int64_t n_tris, 
     if (remap[i] < 0) continue;
     const mcpt_bvh_node &b = nodes[i], &L = nodes[b.left], &R = nodes[b.right];
     DevNode &d = dn[remap[i]];
-    d.a = (f4){L.bbmin[0], L.bbmin[1], L.bbmin[2], L.bbmax[0]};
-    d.b = (f4){L.bbmax[1], L.bbmax[2], R.bbmin[0], R.bbmin[1]};
-    d.c = (f4){R.bbmin[2], R.bbmax[0], R.bbmax[1], R.bbmax[2]};
+    d.a = (f4){L.bbmin[0], L.bbmax[0], L.bbmin[1], L.bbmax[1]};
+    d.b = (f4){L.bbmin[2], L.bbmax[2], R.bbmin[0], R.bbmax[0]};
+    d.c = (f4){R.bbmin[1], R.bbmax[1], R.bbmin[2], R.bbmax[2]};
     d.left = child(b.left);
     d.right = child(b.right);
   }
   if (n_int > 0 && remap[0] != 0) return mcpt::fail(MCPT_ERR_ARG, "scene_upload: root must be node 0");
+  // 4-wide collapse (DevNode4): breadth-first over the binary internal nodes
+  // that start a 4-wide node (the root and every internal grandchild).
+  std::vector<DevNode4> dn4;
+  int32_t depth4 = 1;
+  if (n_int > 0) {
+    std::vector<int32_t> order(1, 0);  // binary ids of 4-wide nodes, index = DevNode4 id
+    std::vector<int32_t> need;         // stack entries needed below each 4-wide node
+    for (size_t k = 0; k < order.size(); ++k) {
+      const mcpt_bvh_node &b = nodes[order[k]];
+      DevNode4 q;
+      std::memset(&q, 0, sizeof(q));
+      int slot = 0;
+      auto put = [&](int32_t c) {
+        const mcpt_bvh_node &x = nodes[c];
+        float v[6] = {x.bbmin[0], x.bbmax[0], x.bbmin[1], x.bbmax[1], x.bbmin[2], x.bbmax[2]};
+        float *qf = reinterpret_cast<float *>(q.q);
+        std::memcpy(qf + 6 * slot, v, sizeof(v));
+        if (x.left == x.right) {
+          q.link[slot] = ~x.left;
+        } else {
+          q.link[slot] = (int32_t)order.size();
+          order.push_back(c);
+        }
+        ++slot;
+      };
+      for (int32_t c : {b.left, b.right}) {
+        const mcpt_bvh_node &x = nodes[c];
+        if (x.left == x.right) {
+          put(c);
+        } else {
+          put(x.left);
+          put(x.right);
+        }
+      }
+      for (; slot < 4; ++slot) q.link[slot] = kEmptySlot;
+      dn4.push_back(q);
+    }
+    // stack need: visiting slot i of a k-slot node leaves k-1-i entries pending
+    need.assign(dn4.size(), 0);
+    for (int64_t k = (int64_t)dn4.size() - 1; k >= 0; --k) {  // children have larger ids
+      int ns = 0;
+      while (ns < 4 && dn4[k].link[ns] != kEmptySlot) ++ns;
+      int best = ns - 1;
+      for (int i = 0; i < ns; ++i)
+        if (dn4[k].link[i] >= 0) best = std::max(best, ns - 1 - i + need[dn4[k].link[i]]);
+      need[k] = best;
+    }
+    depth4 = std::max(need[0], 1);
+    if (depth4 > 192) return mcpt::fail(MCPT_ERR_LIMIT, "scene_upload: 4-wide stack too deep");
+  } else {
+    dn4.resize(1);
+    std::memset(dn4.data(), 0, sizeof(DevNode4));
+  }
   std::vector<DevTri> dt(n);
   for (int64_t i = 0; i < n; ++i) {
     const mcpt_triangle &t = tris[i];
@@ -773,13 +915,15 @@ int mcpt_scene_upload(mcpt_ctx *ctx, const mcpt_triangle *tris, int64_t n_tris, 
   HIP_OK(hipSetDevice(ctx->device));
   mcpt_scene *s = new mcpt_scene();
   s->device = ctx->device;
-  if (hipMalloc(&s->nodes, dn.size() * sizeof(DevNode)) != hipSuccess ||
+  if (hipMalloc(&s->nodes4, dn4.size() * sizeof(DevNode4)) != hipSuccess ||
+      hipMalloc(&s->nodes, dn.size() * sizeof(DevNode)) != hipSuccess ||
       hipMalloc(&s->tris, dt.size() * sizeof(DevTri)) != hipSuccess ||
       hipMalloc(&s->mats, n_mats * sizeof(mcpt_material)) != hipSuccess) {
     mcpt_scene_destroy(s);
     return mcpt::fail(MCPT_ERR_HIP, "scene_upload: hipMalloc failed");
   }
-  if (hipMemcpy(s->nodes, dn.data(), dn.size() * sizeof(DevNode), hipMemcpyHostToDevice) != hipSuccess ||
+  if (hipMemcpy(s->nodes4, dn4.data(), dn4.size() * sizeof(DevNode4), hipMemcpyHostToDevice) != hipSuccess ||
+      hipMemcpy(s->nodes, dn.data(), dn.size() * sizeof(DevNode), hipMemcpyHostToDevice) != hipSuccess ||
       hipMemcpy(s->tris, dt.data(), dt.size() * sizeof(DevTri), hipMemcpyHostToDevice) != hipSuccess ||
       hipMemcpy(s->mats, mats, n_mats * sizeof(mcpt_material), hipMemcpyHostToDevice) != hipSuccess) {
     mcpt_scene_destroy(s);
@@ -789,8 +933,10 @@ int mcpt_scene_upload(mcpt_ctx *ctx, const mcpt_triangle *tris, int64_t n_tris, 
   s->n_internal = n_int;
   s->n_mats = n_mats;
   s->stack_depth = std::max(depth, 1);
+  s->stack_depth4 = depth4;
   SceneView &v = s->view;
   v.nodes = s->nodes;
+  v.nodes4 = s->nodes4;
   v.tris = s->tris;
   v.mats = s->mats;
   v.root_min = (f4){root.bbmin[0], root.bbmin[1], root.bbmin[2], root.bbmin[3]};
@@ -806,6 +952,7 @@ int mcpt_scene_destroy(mcpt_scene *s) {
   if (!s) return MCPT_OK;
   (void)hipSetDevice(s->device);
   if (s->nodes) (void)hipFree(s->nodes);
+  if (s->nodes4) (void)hipFree(s->nodes4);
   if (s->tris) (void)hipFree(s->tris);
   if (s->mats) (void)hipFree(s->mats);
   delete s;
@@ -857,7 +1004,8 @@ int mcpt_render_frames(mcpt_ctx *ctx, const mcpt_scene *scene, const mcpt_camera
     if (std::sscanf(e, "%d,%d", &a, &b) == 2 && a >= 1 && b >= 1) A.th_leaf = a, A.th_shade = b;
   }
   const int64_t tiles = (int64_t)A.tiles_x * ((A.local_rows + 7) / 8);
-  const size_t lds = (size_t)scene->stack_depth * 64 * sizeof(int32_t);
+  const int depth_entries = p->mode == MCPT_MODE_NOPRUNE ? scene->stack_depth : scene->stack_depth4;
+  const size_t lds = (size_t)depth_entries * 64 * sizeof(int32_t);
   int fpl = p->frames_per_launch;
   if (fpl <= 0) {  // aim for ~2^26 lane-frames per launch: long enough to amortise, short enough to stream
     int64_t px = (int64_t)p->width * A.local_rows;
@@ -940,7 +1088,7 @@ int mcpt_intersect(mcpt_ctx *ctx, const mcpt_scene *scene, const mcpt_ray *rays,
   if (!ctx || !scene || !rays || !hits || n < 0) return mcpt::fail(MCPT_ERR_ARG, "intersect: bad argument");
   if (n == 0) return MCPT_OK;
   HIP_OK(hipSetDevice(ctx->device));
-  size_t lds = (size_t)scene->stack_depth * 64 * sizeof(int32_t);
+  size_t lds = (size_t)(mode == MCPT_MODE_NOPRUNE ? scene->stack_depth : scene->stack_depth4) * 64 * sizeof(int32_t);
   dim3 g((unsigned)((n + 63) / 64));
   if (mode == MCPT_MODE_NOPRUNE)
     hipLaunchKernelGGL(k_intersect<MCPT_MODE_NOPRUNE>, g, dim3(64), lds, (hipStream_t)stream, scene->view, rays, n,
