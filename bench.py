@@ -36,10 +36,17 @@ sys.path.insert(0, ROOT)
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
-W = 1024
-H_PER_GPU = 1024
-DEPTH = 8
 STRIPE_ROWS = 16
+# BASELINE.json configs: the headline is C2; C3/C5 are extra bench lines (--workload)
+WORKLOADS = {
+    "C2": {"desc": "C2: cbox 1024x1024/GPU, 8 bounces, diffuse-only, 1 sample/pixel/step",
+           "w": 1024, "h": 1024, "depth": 8},
+    "C3": {"desc": "C3: veach_mis 1024x1024/GPU, 12 bounces, glossy+emitters, 1 sample/pixel/step",
+           "w": 1024, "h": 1024, "depth": 12},
+    "C5": {"desc": "C5: 10M random triangles, 2048x2048/GPU, 8 bounces, 1 sample/pixel/step",
+           "w": 2048, "h": 2048, "depth": 8},
+}
+W, H_PER_GPU, DEPTH = 1024, 1024, 8
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 METRIC = "Msamples/s (rays traced x bounces / s) at 1024x1024"
 
@@ -51,21 +58,29 @@ def dist_env():
     return ws, rank, local
 
 
-def load_scene():
-    from montecarlopathtracing_amd import scene as S
-    return S.SceneData.from_obj(os.path.join(ROOT, "scenes/cbox/"), "cbox.obj", material_override=S.diffuse_only)
-
-
 CBOX_CAM = {"position": [278, 273, -800], "lookat": [278, 273, -799], "up": [0, 1, 0], "fov": 39.3077}
+MIS_CAM = {"position": [0, 2, 15], "lookat": [0, -2, 2.5], "up": [0, 1, 0], "fov": 28}
 
 
-def e_counts():
+def load_scene(workload):
+    from montecarlopathtracing_amd import scene as S
+    if workload == "C2":
+        return S.SceneData.from_obj(os.path.join(ROOT, "scenes/cbox/"), "cbox.obj",
+                                    material_override=S.diffuse_only), CBOX_CAM
+    if workload == "C3":
+        return S.SceneData.from_obj(os.path.join(ROOT, "scenes/veach_mis/"), "mis.obj"), MIS_CAM
+    if workload == "C5":
+        return S.random_mesh(10_000_000), S.RANDOM_MESH_CAMERA
+    raise ValueError(workload)
+
+
+def e_counts(workload="C2"):
     """E_node / E_tri (per active segment) of the t-pruned, left-first
     reference traversal, measured once by the CPU oracle
     (tests/measure_e_counts.py) and committed in profiles/e_counts.json."""
     try:
         with open(os.path.join(ROOT, "profiles", "e_counts.json")) as fh:
-            return json.load(fh).get("C2")
+            return json.load(fh).get(workload)
     except (OSError, ValueError):
         return None
 
@@ -75,7 +90,7 @@ def default_seeds(n):
     return ds(n)
 
 
-def cpu_baseline(data, cam, h_img, target_s=12.0):
+def cpu_baseline(data, cam, h_img, target_s=15.0):
     """The CPU oracle on a bounded sample: every k-th pixel of the same image,
     same depth, frames scaled so the sample takes ~target_s seconds."""
     from tests import oracle as O
@@ -88,7 +103,7 @@ def cpu_baseline(data, cam, h_img, target_s=12.0):
     t0 = time.time()
     O.render(data, cam, W, h_img, DEPTH, 1, 1 << 20, seeds, pixels=px[:2048], threads=threads)
     probe = max(time.time() - t0, 1e-3)
-    frames = int(max(1, min(64, target_s / (probe * len(px) / 2048.0))))
+    frames = int(max(1, min(4096, target_s / (probe * len(px) / 2048.0))))
     t0 = time.time()
     _, _, _, st = O.render(data, cam, W, h_img, DEPTH, frames, 1 << 20, seeds, pixels=px, threads=threads)
     dt = time.time() - t0
@@ -118,7 +133,11 @@ def main():
     ap.add_argument("--warmup", type=int, default=4)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--frames-per-launch", type=int, default=16)
+    ap.add_argument("--workload", default="C2", choices=sorted(WORKLOADS))
     args = ap.parse_args()
+    global W, H_PER_GPU, DEPTH
+    wl = WORKLOADS[args.workload]
+    W, H_PER_GPU, DEPTH = wl["w"], wl["h"], wl["depth"]
 
     ws, rank, local = dist_env()
     n = max(ws, 1)
@@ -131,8 +150,8 @@ def main():
     from montecarlopathtracing_amd import scene as S
 
     h_img = H_PER_GPU * n
-    data = load_scene()
-    cam = S.parse_camera(CBOX_CAM)
+    data, camj = load_scene(args.workload)
+    cam = S.parse_camera(camj)
     rnd = R.Renderer(local if ws > 1 else 0)
     dsc = rnd.upload(data)
     seeds = default_seeds(W * h_img)
@@ -175,7 +194,7 @@ def main():
     value = total_samples / elapsed / 1e6
     out = None
     if rank == 0:
-        ec = e_counts()
+        ec = e_counts(args.workload)
         roof = None
         if ec:
             b_seg = 328.0 + 64.0 * (ec["E_node"] + ec["E_tri"])
@@ -191,13 +210,14 @@ def main():
                     "kernel_node_fetches_per_seg": round(cst["node_visits"] / max(segments, 1), 3),
                     "kernel_tri_tests_per_seg": round(cst["tri_tests"] / max(segments, 1), 3)}
         cpu = None
-        if n == 1 and not args.no_cpu:
+        if n == 1 and not args.no_cpu and args.workload == "C2":
             cpu = cpu_baseline(data, cam, h_img)
         out = {"metric": METRIC, "value": round(value, 2), "unit": "Msamples/s", "n_gpus": n, "steps": args.steps,
                "warmup": args.warmup, "ms_per_step": round(elapsed * 1e3 / args.steps, 4),
                "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
-               "data": "synthetic seeds; Scene/cbox geometry recovered from the reference's cbox.mb",
-               "config": {"workload": "C2: cbox 1024x1024/GPU, 8 bounces, diffuse-only, 1 sample/pixel/step",
+               "data": "synthetic seeds; " + ("Scene/cbox geometry recovered from the reference's cbox.mb"
+                                              if args.workload == "C2" else "see config.workload"),
+               "config": {"workload": wl["desc"],
                           "width": W, "height_per_gpu": H_PER_GPU, "max_depth": DEPTH,
                           "parallelism": "row-stripe tiles x%d" % n, "mode": "exact"},
                "active_Msegments_per_s": round(segments * n / elapsed / 1e6, 2),

@@ -444,6 +444,7 @@ struct RenderArgs {
   int32_t stack_depth;
   int32_t th_leaf, th_shade;  // lanes waiting before the L / S phase runs
   int32_t *queue;             // pixel work-queue head (zeroed before each launch)
+  int32_t lds_mats;           // 1: copy the material table to LDS after the stack
 };
 
 __device__ inline int32_t global_row(int32_t lr, const RenderArgs &A) {
@@ -479,6 +480,14 @@ __global__ void __launch_bounds__(64, MCPT_WAVES_PER_SIMD) k_render(RenderArgs A
   const int lane = threadIdx.x;
   int32_t *stk = lds_stack + lane;  // column-major [depth][64]: conflict-free
   const SceneView &S = A.S;
+  // material table copied to LDS behind the stack (small tables only)
+  const mcpt_material *mats = S.mats;
+  if (A.lds_mats) {
+    mcpt_material *lm = reinterpret_cast<mcpt_material *>(lds_stack + A.stack_depth * 64);
+    for (int k = lane; k < S.n_mats; k += 64) lm[k] = S.mats[k];
+    __syncthreads();
+    mats = lm;
+  }
 
   unsigned long long n_seg = 0, n_nodes = 0, n_tests = 0, n_bad = 0;
   unsigned long long w_t = 0, w_l = 0, w_s = 0;
@@ -500,13 +509,13 @@ __global__ void __launch_bounds__(64, MCPT_WAVES_PER_SIMD) k_render(RenderArgs A
   // path / traversal state (declared with the pixel state below)
   f3 rinv = (f3){0.0f, 0.0f, 0.0f};
   float best_t = kFltMax;
-  int32_t best_tri = -1, cur = kDone, sp = 0;
+  int32_t cur = kDone, sp = 0;
+  f4 best_nrm = (f4){0.0f, 0.0f, 0.0f, 0.0f};  // hit triangle's packed normal, kept from the L phase
   auto begin_segment = [&]() {
     rinv.x = __builtin_amdgcn_rcpf(d.x);
     rinv.y = __builtin_amdgcn_rcpf(d.y);
     rinv.z = __builtin_amdgcn_rcpf(d.z);
     best_t = kFltMax;
-    best_tri = -1;
     sp = 0;
     if (slab_pass(box_test<LIT>(S.root_min.xyz, S.root_max.xyz, o.xyz, d.xyz, rinv), kTmin))
       cur = S.root_leaf >= 0 ? ~S.root_leaf : 0;
@@ -592,7 +601,7 @@ __global__ void __launch_bounds__(64, MCPT_WAVES_PER_SIMD) k_render(RenderArgs A
         if (STATS) n_tests++;
         if (h.accept && best_t - h.t >= kEps) {  // objdef.h:213 — first-found wins near-ties
           best_t = h.t;
-          best_tri = id;
+          best_nrm = T.nrm;
         }
         cur = sp == 0 ? kDone : stk[(--sp) * 64];
       }
@@ -609,7 +618,7 @@ __global__ void __launch_bounds__(64, MCPT_WAVES_PER_SIMD) k_render(RenderArgs A
           color = (f4){0.0f, 0.0f, 0.0f, 0.0f};
           done = true;
         } else {
-          const f4 tn = S.tris[best_tri].nrm;
+          const f4 tn = best_nrm;
           ShadeIn in;
           in.o = o;
           in.d = d;
@@ -617,7 +626,7 @@ __global__ void __launch_bounds__(64, MCPT_WAVES_PER_SIMD) k_render(RenderArgs A
           if (cl_dot3(d.xyz, in.nrm.xyz) > 0) in.nrm = -in.nrm;  // intersect.cl:23-25
           in.pt = o + best_t * d;                                  // objdef.h:218
           in.mat = as_i(tn.w);
-          ShadeOut so = shade_hit(S.mats, in, color, seed, A.max_depth);
+          ShadeOut so = shade_hit(mats, in, color, seed, A.max_depth);
           if (STATS) n_bad += so.bad;
           color = so.color;
           o = so.o;
@@ -1005,7 +1014,9 @@ int mcpt_render_frames(mcpt_ctx *ctx, const mcpt_scene *scene, const mcpt_camera
   }
   const int64_t tiles = (int64_t)A.tiles_x * ((A.local_rows + 7) / 8);
   const int depth_entries = p->mode == MCPT_MODE_NOPRUNE ? scene->stack_depth : scene->stack_depth4;
-  const size_t lds = (size_t)depth_entries * 64 * sizeof(int32_t);
+  A.stack_depth = depth_entries;
+  A.lds_mats = scene->n_mats <= 256 ? 1 : 0;
+  const size_t lds = (size_t)depth_entries * 64 * sizeof(int32_t) + (A.lds_mats ? scene->n_mats * sizeof(mcpt_material) : 0);
   int fpl = p->frames_per_launch;
   if (fpl <= 0) {  // aim for ~2^26 lane-frames per launch: long enough to amortise, short enough to stream
     int64_t px = (int64_t)p->width * A.local_rows;

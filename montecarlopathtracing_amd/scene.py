@@ -124,3 +124,28 @@ def diffuse_only(mats):
         if m[i]["type"] != L.MCPT_LIGHT:
             m[i]["type"] = L.MCPT_DIFFUSE
     return m
+
+
+# ------------------------------------------------------------- synthetic scenes
+RANDOM_MESH_CAMERA = {"position": [50.0, 50.0, -150.0], "lookat": [50.0, 50.0, 50.0], "up": [0, 1, 0], "fov": 45.0}
+
+
+def random_mesh(n, seed=42, extent=100.0):
+    """BASELINE.json configs[4] / SURVEY.md §8(d) C5: n random triangles,
+    centres uniform in [0, extent]^3, corners = centre + U[-h, h]^3 with
+    h = 0.5 * extent / n^(1/3); diffuse 0.5; one emissive quad (Ka 10)
+    above the volume.  numpy PCG64(seed) stands in for the survey's PCG32."""
+    rng = np.random.Generator(np.random.PCG64(seed))
+    h = 0.5 * extent / float(n) ** (1.0 / 3.0)
+    c = rng.uniform(0.0, extent, (n, 1, 3)).astype(np.float32)
+    v = (c + rng.uniform(-h, h, (n, 3, 3)).astype(np.float32)).astype(np.float32)
+    y = np.float32(1.2 * extent)
+    lo, hi = np.float32(0.25 * extent), np.float32(0.75 * extent)
+    quad = np.array([[[lo, y, lo], [hi, y, lo], [hi, y, hi]], [[lo, y, lo], [hi, y, hi], [lo, y, hi]]], np.float32)
+    verts = np.concatenate([v, quad], axis=0)
+    mat_index = np.zeros(len(verts), np.int32)
+    mat_index[-2:] = 1
+    mats = np.zeros(2, L.MATERIAL)
+    mats[0] = classify_material(1.0, (0, 0, 0), (0.5, 0.5, 0.5), (0, 0, 0), 1.0)
+    mats[1] = classify_material(1.0, (10, 10, 10), (0, 0, 0), (0, 0, 0), 1.0)
+    return SceneData.from_arrays(verts, mat_index, mats)

@@ -24,6 +24,7 @@ CONFIGS = {
     "C1": (scenes.cbox, scenes.CBOX_CAM, 256, 256, 4),
     "C2": (scenes.cbox_diffuse, scenes.CBOX_CAM, 1024, 1024, 8),
     "C3": (scenes.mis, scenes.MIS_CAM, 1024, 1024, 12),
+    "C5": (lambda: S.random_mesh(10_000_000), S.RANDOM_MESH_CAMERA, 2048, 2048, 8),
 }
 
 
