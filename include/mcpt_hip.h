@@ -127,7 +127,7 @@ typedef struct mcpt_render_params {
 
 typedef struct mcpt_stats {
   uint64_t segments;                /* rays alive at intersect entry, all frames */
-  uint64_t node_visits;             /* BVH nodes whose children were tested */
+  uint64_t node_visits;             /* nodes whose children were tested (EXACT: 4-wide) */
   uint64_t tri_tests;               /* triangle tests                        */
   uint64_t bad_material;            /* hits on an unknown material type      */
   double   kernel_ms;               /* device time of the last render call   */
@@ -136,6 +136,8 @@ typedef struct mcpt_stats {
   uint64_t wave_node_phases;        /* wave-level node steps (SIMT efficiency = */
   uint64_t wave_leaf_phases;        /*  node_visits / (64 * wave_node_phases)) */
   uint64_t wave_shade_phases;
+  uint64_t order_fallbacks;         /* EXACT: segments re-searched in the     */
+                                    /*  reference's left-first order         */
 } mcpt_stats;
 
 /* ------------------------------------------------------- version / errors */
@@ -226,6 +228,12 @@ int mcpt_accumulate(mcpt_ctx *ctx, float *color_dev, float *hist_dev, int32_t *c
 /* Counters of the last render call (segments etc. need stats enabled).   */
 int mcpt_set_stats(mcpt_ctx *ctx, int32_t enabled);
 int mcpt_get_stats(mcpt_ctx *ctx, mcpt_stats *out);
+
+/* Device self-check of the inline sin/cos used by randomDirection
+ * (shade.cl:40-59) against the ocml library calls the reference kernel
+ * makes: mismatching bit patterns over the 32768 angles 2*pi*r/32768 and
+ * over every float in [0, 8). Both counts are 0 on a correct build.       */
+int mcpt_selfcheck_trig(mcpt_ctx *ctx, int64_t *angle_mismatches, int64_t *range_mismatches);
 
 #ifdef __cplusplus
 }

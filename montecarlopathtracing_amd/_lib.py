@@ -44,7 +44,7 @@ class Stats(ctypes.Structure):
                 ("tri_tests", ctypes.c_uint64), ("bad_material", ctypes.c_uint64),
                 ("kernel_ms", ctypes.c_double), ("launches", ctypes.c_int32), ("pad", ctypes.c_int32),
                 ("wave_node_phases", ctypes.c_uint64), ("wave_leaf_phases", ctypes.c_uint64),
-                ("wave_shade_phases", ctypes.c_uint64)]
+                ("wave_shade_phases", ctypes.c_uint64), ("order_fallbacks", ctypes.c_uint64)]
 
 
 class MCPTError(RuntimeError):
@@ -82,6 +82,7 @@ SIGNATURES = {
     "mcpt_accumulate": (_I32, [_P, _P, _P, _P, _I64, _I32, _P]),
     "mcpt_set_stats": (_I32, [_P, _I32]),
     "mcpt_get_stats": (_I32, [_P, _P]),
+    "mcpt_selfcheck_trig": (_I32, [_P, _P, _P]),
 }
 
 _lib = None

@@ -25,10 +25,12 @@
 #include <cmath>
 #include <cstring>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/mcpt_hip.h"
 #include "mcpt_refmath.h"
+#include "mcpt_bvh4.h"
 
 using namespace mcpt;
 
@@ -73,13 +75,15 @@ struct __attribute__((aligned(16))) DevNode4 {
   int32_t link[4];  // >= 0 internal DevNode4, < 0 leaf ~triangle, kEmptySlot unused
   f4 pad;
 };
-static_assert(sizeof(DevNode4) == 128, "128-B 4-wide node");
+static_assert(sizeof(DevNode4) == 128 && sizeof(DevNode4) == sizeof(mcpt::Node4Rec), "128-B 4-wide node");
 constexpr int32_t kDone = INT32_MIN;           // traversal finished
 constexpr int32_t kPop = INT32_MIN + 1;        // take the next entry from the stack
 constexpr int32_t kEmptySlot = INT32_MIN + 2;  // unused 4-wide slot
+static_assert(kEmptySlot == mcpt::kEmptySlot4, "one empty-slot marker");
 
 struct SceneView {
-  const DevNode4 *nodes4;
+  const DevNode4 *near4;   // EXACT search tree (binned SAH, nearest-first; mcpt_sah.cpp)
+  const DevNode4 *nodes4;  // the reference HLBVH collapsed 4-wide (left-first fallback)
   const DevNode *nodes;
   const DevTri *tris;
   const mcpt_material *mats;
@@ -91,8 +95,9 @@ struct SceneView {
 
 struct mcpt_scene {
   int device;
+  DevNode4 *near4 = nullptr;
   DevNode4 *nodes4 = nullptr;
-  int32_t stack_depth4 = 1;
+  int32_t stack_depth4 = 1;  // EXACT: max of both 4-wide trees' stack needs
   DevNode *nodes = nullptr;
   DevTri *tris = nullptr;
   mcpt_material *mats = nullptr;
@@ -163,12 +168,15 @@ __device__ inline void child_boxes(const DevNode &N, f3 o, f3 d, f3 rinv, BoxT &
   }
 }
 
-// One 4-wide node: slab test of the 4 slots, then left-first order.
-// Returns the next entry (internal node, leaf, or kPop) and pushes the other
-// passing slots so that they pop in slot order.
+// One 4-wide node: slab test of the 4 slots, then pick the slot to enter.
+// NEAREST (the SAH search tree): the passing slot with the smallest entry
+// distance, ties to the lower slot; otherwise (the reference tree) the lowest
+// passing slot, i.e. the reference's left-first DFS.  The other passing slots
+// are pushed so that they pop in slot order.  Returns the slot's link (an
+// internal node or ~triangle) or kPop.
 template <bool PRUNE>
-__device__ inline int32_t step4(const DevNode4 &N, f3 o, f3 rinv, float tmin, float lim, int32_t *stk, int &sp,
-                                uint32_t &nodes_ctr) {
+__device__ inline int32_t step4(const DevNode4 &N, f3 o, f3 rinv, float tmin, float lim, bool nearest, int32_t *stk,
+                                int &sp, int stride, uint32_t &nodes_ctr) {
   const f4 q0 = N.q[0], q1 = N.q[1], q2 = N.q[2], q3 = N.q[3], q4 = N.q[4], q5 = N.q[5];
   BoxT b0 = slab_pairs(q0.xy, q0.zw, q1.xy, o, rinv);
   BoxT b1 = slab_pairs(q1.zw, q2.xy, q2.zw, o, rinv);
@@ -184,51 +192,46 @@ __device__ inline int32_t step4(const DevNode4 &N, f3 o, f3 rinv, float tmin, fl
     h3 = h3 && !(b3.tnear > lim);
   }
   nodes_ctr++;
+  // left-first: every key 0, so the lowest passing slot wins the <= chain
+  const float k0 = nearest ? b0.tnear : 0.0f, k1 = nearest ? b1.tnear : 0.0f;
+  const float k2 = nearest ? b2.tnear : 0.0f, k3 = nearest ? b3.tnear : 0.0f;
   int32_t nxt = kPop;
-  if (h3) nxt = l3;
-  if (h2) {
-    if (nxt != kPop) stk[(sp++) * 64] = nxt;
-    nxt = l2;
-  }
-  if (h1) {
-    if (nxt != kPop) stk[(sp++) * 64] = nxt;
-    nxt = l1;
-  }
-  if (h0) {
-    if (nxt != kPop) stk[(sp++) * 64] = nxt;
-    nxt = l0;
-  }
+  int sel = 4;
+  float kb = __builtin_inff();
+  if (h3) kb = k3, nxt = l3, sel = 3;
+  if (h2 && !(k2 > kb)) kb = k2, nxt = l2, sel = 2;
+  if (h1 && !(k1 > kb)) kb = k1, nxt = l1, sel = 1;
+  if (h0 && !(k0 > kb)) nxt = l0, sel = 0;
+  if (h3 && sel != 3) stk[(sp++) * stride] = l3;
+  if (h2 && sel != 2) stk[(sp++) * stride] = l2;
+  if (h1 && sel != 1) stk[(sp++) * stride] = l1;
+  if (h0 && sel != 0) stk[(sp++) * stride] = l0;
   return nxt;
 }
 
-template <bool LITERAL>
-__device__ inline void test_tri(const DevTri *__restrict__ tris, int32_t id, f3 o, f3 d, float tmin,
-                                Trace &tr) {
-  const DevTri T = tris[id];
-  TriHit h = LITERAL ? cramer(d, T.nab.xyz, T.nac.xyz, T.v0.xyz - o, T.nrm.xyz, tmin)
-                     : cramer_reduced(d, T.nab.xyz, T.nac.xyz, T.v0.xyz - o, T.nrm.xyz, T.v0.w, T.nab.w,
-                                      T.nac.w, tmin);
-  tr.tests++;
-  if (h.accept) {
-    tr.last = id;
-    if (tr.t - h.t >= kEps) {  // objdef.h:213 — first-found wins near-ties
-      tr.t = h.t;
-      tr.tri = id;
-    }
-  }
+// Result rule of the EXACT search.  The reference keeps the
+// first triangle in its DFS order and replaces it only by one at least EPS
+// closer (objdef.h:213).  Searching in another order, track the closest
+// accepted t1 and the runner-up t2: if every other accepted triangle lies at
+// least EPS behind t1 (t2 - t1 >= EPS in the reference's float arithmetic),
+// the t1 triangle replaces whatever the reference holds when it reaches it
+// and nothing replaces it afterwards, so it IS the reference's answer in any
+// order.  Otherwise the ray is re-searched in the reference's own order.
+__device__ inline void near_update(float t, float &t1, float &t2) {  // selects, not branches
+  const bool lt1 = t < t1, lt2 = t < t2;
+  t2 = lt1 ? t1 : (lt2 ? t : t2);
+  t1 = lt1 ? t : t1;
 }
+__device__ inline bool near_ambiguous(float t1, float t2) { return t2 < kFltMax && !(t2 - t1 >= kEps); }
 
-// Left-first DFS of objdef.h:240-275.  PRUNE skips a child whose box starts
-// farther than the current hit plus a margin: every triangle inside it would
-// have t > hit.t and could not replace the hit.
+// NOPRUNE: the reference's exhaustive left-first DFS of objdef.h:240-275 on
+// its binary tree with the literal division.
 //
 // SIMT shape ("while-while", Aila & Laine 2009): the inner loop walks internal
 // nodes until EVERY lane of the wave holds a leaf (or is done); then all lanes
 // with a leaf run the Cramer test together.  Each lane still tests its
 // triangles in exactly the reference's DFS order.
-
-template <bool PRUNE, bool LITERAL>
-__device__ inline Trace traverse(const SceneView &S, f3 o, f3 d, float tmin, int32_t *stk, int stride) {
+__device__ inline Trace traverse_noprune(const SceneView &S, f3 o, f3 d, float tmin, int32_t *stk, int stride) {
   Trace tr;
   tr.t = kFltMax;
   tr.tri = -1;
@@ -240,38 +243,90 @@ __device__ inline Trace traverse(const SceneView &S, f3 o, f3 d, float tmin, int
   rinv.y = __builtin_amdgcn_rcpf(d.y);
   rinv.z = __builtin_amdgcn_rcpf(d.z);
   int32_t cur;  // >= 0 internal node, kDone, or ~triangle (a leaf waiting for its test)
-  if (!slab_pass(box_test<LITERAL>(S.root_min.xyz, S.root_max.xyz, o, d, rinv), tmin))
+  if (!slab_pass(box_test<true>(S.root_min.xyz, S.root_max.xyz, o, d, rinv), tmin))
     cur = kDone;
   else
     cur = S.root_leaf >= 0 ? ~S.root_leaf : 0;
   const DevNode *__restrict__ nodes = S.nodes;
   int sp = 0;
   while (cur != kDone) {
-    // ---- walk internal nodes until this lane holds a leaf or is done
     while (cur >= 0) {
-      if (!LITERAL) {  // 4-wide collapsed tree (same DFS order)
-        cur = step4<PRUNE>(S.nodes4[cur], o, rinv, tmin, tr.t + S.prune_margin, stk, sp, tr.nodes);
-      } else {
-        const DevNode N = nodes[cur];
-        tr.nodes++;
-        BoxT bl, br;
-        child_boxes<LITERAL>(N, o, d, rinv, bl, br);
-        bool hl = slab_pass(bl, tmin), hr = slab_pass(br, tmin);
-        if (PRUNE) {
-          const float lim = tr.t + S.prune_margin;
-          hl = hl && !(bl.tnear > lim);
-          hr = hr && !(br.tnear > lim);
-        }
-        if (hl && hr) stk[(sp++) * stride] = N.right;  // reference: push right, descend left
-        cur = hl ? N.left : (hr ? N.right : kPop);
-      }
+      const DevNode N = nodes[cur];
+      tr.nodes++;
+      BoxT bl, br;
+      child_boxes<true>(N, o, d, rinv, bl, br);
+      const bool hl = slab_pass(bl, tmin), hr = slab_pass(br, tmin);
+      if (hl && hr) stk[(sp++) * stride] = N.right;  // reference: push right, descend left
+      cur = hl ? N.left : (hr ? N.right : kPop);
       if (cur == kPop) cur = sp == 0 ? kDone : stk[(--sp) * stride];
     }
-    // ---- all lanes: test the pending leaf, then continue from the stack
     if (cur != kDone) {
-      test_tri<LITERAL>(S.tris, ~cur, o, d, tmin, tr);
+      const int32_t id = ~cur;
+      const DevTri T = S.tris[id];
+      const TriHit h = cramer(d, T.nab.xyz, T.nac.xyz, T.v0.xyz - o, T.nrm.xyz, tmin);
+      tr.tests++;
+      if (h.accept) {
+        tr.last = id;
+        if (tr.t - h.t >= kEps) {  // objdef.h:213 — first-found wins near-ties
+          tr.t = h.t;
+          tr.tri = id;
+        }
+      }
       cur = sp == 0 ? kDone : stk[(--sp) * stride];
     }
+  }
+  return tr;
+}
+
+// EXACT: nearest-first search of the SAH tree under the result rule above;
+// a ray whose answer could depend on the order is searched again left-first
+// on the reference tree with the reference's rule.  Both searches skip a
+// child whose box starts farther than the current hit plus a margin: every
+// triangle inside it lies behind the hit.
+__device__ inline Trace traverse_exact(const SceneView &S, f3 o, f3 d, float tmin, int32_t *stk, int stride,
+                                       uint32_t &fallbacks) {
+  Trace tr;
+  tr.nodes = 0;
+  tr.tests = 0;
+  f3 rinv;
+  rinv.x = __builtin_amdgcn_rcpf(d.x);
+  rinv.y = __builtin_amdgcn_rcpf(d.y);
+  rinv.z = __builtin_amdgcn_rcpf(d.z);
+  const bool enter = slab_pass(slab(S.root_min.xyz, S.root_max.xyz, o, rinv), tmin);
+  for (int pass = 0;; ++pass) {
+    const bool ref = pass > 0;
+    const DevNode4 *__restrict__ tree = ref ? S.nodes4 : S.near4;
+    tr.t = kFltMax;
+    tr.tri = -1;
+    tr.last = -1;
+    float t2 = kFltMax;
+    int32_t cur = !enter ? kDone : (S.root_leaf >= 0 ? ~S.root_leaf : 0);
+    int sp = 0;
+    while (cur != kDone) {
+      while (cur >= 0) {
+        cur = step4<true>(tree[cur], o, rinv, tmin, tr.t + S.prune_margin, !ref, stk, sp, stride, tr.nodes);
+        if (cur == kPop) cur = sp == 0 ? kDone : stk[(--sp) * stride];
+      }
+      if (cur != kDone) {
+        const int32_t id = ~cur;
+        const DevTri T = S.tris[id];
+        const TriHit h = cramer_reduced(d, T.nab.xyz, T.nac.xyz, T.v0.xyz - o, T.nrm.xyz, T.v0.w, T.nab.w,
+                                        T.nac.w, tmin);
+        tr.tests++;
+        if (h.accept) {
+          tr.last = id;
+          if (ref ? tr.t - h.t >= kEps : h.t < tr.t) tr.tri = id;
+          if (ref) {
+            if (tr.t - h.t >= kEps) tr.t = h.t;
+          } else {
+            near_update(h.t, tr.t, t2);
+          }
+        }
+        cur = sp == 0 ? kDone : stk[(--sp) * stride];
+      }
+    }
+    if (ref || !near_ambiguous(tr.t, t2)) break;
+    fallbacks++;
   }
   return tr;
 }
@@ -490,7 +545,7 @@ __global__ void __launch_bounds__(64, MCPT_WAVES_PER_SIMD) k_render(RenderArgs A
   }
 
   unsigned long long n_seg = 0, n_nodes = 0, n_tests = 0, n_bad = 0;
-  unsigned long long w_t = 0, w_l = 0, w_s = 0;
+  unsigned long long w_t = 0, w_l = 0, w_s = 0, n_fb = 0;
   // pixel state
   bool alive = true;   // queue not exhausted for this lane
   bool has_px = false; // owns a pixel
@@ -511,11 +566,17 @@ __global__ void __launch_bounds__(64, MCPT_WAVES_PER_SIMD) k_render(RenderArgs A
   float best_t = kFltMax;
   int32_t cur = kDone, sp = 0;
   f4 best_nrm = (f4){0.0f, 0.0f, 0.0f, 0.0f};  // hit triangle's packed normal, kept from the L phase
+  // EXACT: ref = searching the reference tree left-first (the fallback of
+  // traverse_exact); t2 = runner-up t of the nearest-first search
+  bool ref = LIT;
+  float t2 = kFltMax;
   auto begin_segment = [&]() {
     rinv.x = __builtin_amdgcn_rcpf(d.x);
     rinv.y = __builtin_amdgcn_rcpf(d.y);
     rinv.z = __builtin_amdgcn_rcpf(d.z);
     best_t = kFltMax;
+    t2 = kFltMax;
+    ref = LIT;
     sp = 0;
     if (slab_pass(box_test<LIT>(S.root_min.xyz, S.root_max.xyz, o.xyz, d.xyz, rinv), kTmin))
       cur = S.root_leaf >= 0 ? ~S.root_leaf : 0;
@@ -566,9 +627,10 @@ __global__ void __launch_bounds__(64, MCPT_WAVES_PER_SIMD) k_render(RenderArgs A
     if (__ballot(in_t)) {
       if (STATS && lane == __builtin_ctzll(__ballot(1))) w_t++;
       if (in_t) {
-        if (!LIT) {  // 4-wide collapsed tree, same DFS order (DevNode4)
+        if (!LIT) {  // EXACT: SAH tree nearest-first, or the reference tree left-first
           uint32_t ctr = 0;
-          cur = step4<PRUNE>(S.nodes4[cur], o.xyz, rinv, kTmin, best_t + S.prune_margin, stk, sp, ctr);
+          const DevNode4 *__restrict__ tree = ref ? S.nodes4 : S.near4;
+          cur = step4<PRUNE>(tree[cur], o.xyz, rinv, kTmin, best_t + S.prune_margin, !ref, stk, sp, 64, ctr);
           if (STATS) n_nodes += ctr;
         } else {  // NOPRUNE: the reference's binary tree, literal division
           const DevNode N = S.nodes[cur];
@@ -599,9 +661,13 @@ __global__ void __launch_bounds__(64, MCPT_WAVES_PER_SIMD) k_render(RenderArgs A
                        : cramer_reduced(d.xyz, T.nab.xyz, T.nac.xyz, T.v0.xyz - o.xyz, T.nrm.xyz, T.v0.w,
                                         T.nab.w, T.nac.w, kTmin);
         if (STATS) n_tests++;
-        if (h.accept && best_t - h.t >= kEps) {  // objdef.h:213 — first-found wins near-ties
-          best_t = h.t;
-          best_nrm = T.nrm;
+        if (h.accept) {
+          if (ref ? best_t - h.t >= kEps : h.t < best_t) best_nrm = T.nrm;  // objdef.h:213
+          if (ref) {
+            if (best_t - h.t >= kEps) best_t = h.t;
+          } else {
+            near_update(h.t, best_t, t2);
+          }
         }
         cur = sp == 0 ? kDone : stk[(--sp) * 64];
       }
@@ -611,7 +677,13 @@ __global__ void __launch_bounds__(64, MCPT_WAVES_PER_SIMD) k_render(RenderArgs A
     const unsigned long long ms = __ballot(in_s);
     if (ms && (__popcll(ms) >= A.th_shade || !__ballot(live && cur != kDone))) {
       if (STATS && lane == __builtin_ctzll(__ballot(1))) w_s++;
-      if (in_s) {
+      if (in_s && !ref && near_ambiguous(best_t, t2)) {  // order could matter: search again left-first
+        if (STATS) n_fb++;
+        ref = true;
+        best_t = kFltMax;
+        sp = 0;
+        cur = S.root_leaf >= 0 ? ~S.root_leaf : 0;  // the root box passed: there were hits
+      } else if (in_s) {
         if (STATS) n_seg++;
         bool done;
         if (best_t >= kFltMax) {  // shade.cl:92-96 — miss: black, terminate
@@ -654,6 +726,7 @@ __global__ void __launch_bounds__(64, MCPT_WAVES_PER_SIMD) k_render(RenderArgs A
     atomicAdd(&A.stats[1], n_nodes);
     atomicAdd(&A.stats[2], n_tests);
     if (n_bad) atomicAdd(&A.stats[3], n_bad);
+    if (n_fb) atomicAdd(&A.stats[7], n_fb);
     if (w_t | w_l | w_s) {
       atomicAdd(&A.stats[4], w_t);
       atomicAdd(&A.stats[5], w_l);
@@ -682,8 +755,9 @@ __global__ void __launch_bounds__(64) k_intersect(SceneView S, const mcpt_ray *r
   const f4 o = *(const f4 *)rays[id].origin;
   const f4 d = *(const f4 *)rays[id].direction;
   if (as_i(o.w) & (int32_t)0xFF000000) return;  // intersect.cl:16-18 (hit left untouched)
-  Trace tr = MODE == MCPT_MODE_NOPRUNE ? traverse<false, true>(S, o.xyz, d.xyz, tmin, lds_stack + threadIdx.x, 64)
-                                       : traverse<true, false>(S, o.xyz, d.xyz, tmin, lds_stack + threadIdx.x, 64);
+  uint32_t fallbacks = 0;
+  Trace tr = MODE == MCPT_MODE_NOPRUNE ? traverse_noprune(S, o.xyz, d.xyz, tmin, lds_stack + threadIdx.x, 64)
+                                       : traverse_exact(S, o.xyz, d.xyz, tmin, lds_stack + threadIdx.x, 64, fallbacks);
   mcpt_hit h;
   f4 nrm = (f4){0.0f, 0.0f, 0.0f, 0.0f}, pt = (f4){0.0f, 0.0f, 0.0f, 0.0f};
   h.t = tr.t;
@@ -786,6 +860,34 @@ int mcpt_ctx_destroy(mcpt_ctx *c) {
   if (c->ev0) (void)hipEventDestroy(c->ev0);
   if (c->ev1) (void)hipEventDestroy(c->ev1);
   delete c;
+  return MCPT_OK;
+}
+
+// sincos_small vs the ocml calls, bit for bit (mcpt_selfcheck_trig).
+__global__ void k_selfcheck_trig(uint32_t n, int angles, unsigned long long *bad) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const float x = angles ? random_phi(i) : __builtin_bit_cast(float, i);
+  float s, c;
+  sincos_small(x, s, c);
+  const bool ok = __builtin_bit_cast(uint32_t, s) == __builtin_bit_cast(uint32_t, cl_sin(x)) &&
+                  __builtin_bit_cast(uint32_t, c) == __builtin_bit_cast(uint32_t, cl_cos(x));
+  if (!ok) atomicAdd(bad, 1ull);
+}
+
+int mcpt_selfcheck_trig(mcpt_ctx *c, int64_t *angle_bad, int64_t *range_bad) {
+  if (!c || !angle_bad || !range_bad) return mcpt::fail(MCPT_ERR_ARG, "selfcheck_trig: null");
+  HIP_OK(hipSetDevice(c->device));
+  HIP_OK(hipMemset(c->d_stats, 0, 2 * sizeof(unsigned long long)));
+  const uint32_t n_range = 0x41000000u;  // bit patterns of [0, 8.0f)
+  hipLaunchKernelGGL(k_selfcheck_trig, dim3(32768 / 256), dim3(256), 0, 0, 32768u, 1, c->d_stats);
+  hipLaunchKernelGGL(k_selfcheck_trig, dim3((n_range + 255) / 256), dim3(256), 0, 0, n_range, 0,
+                     c->d_stats + 1);
+  HIP_OK(hipGetLastError());
+  unsigned long long h[2];
+  HIP_OK(hipMemcpy(h, c->d_stats, sizeof(h), hipMemcpyDeviceToHost));
+  *angle_bad = (int64_t)h[0];
+  *range_bad = (int64_t)h[1];
   return MCPT_OK;
 }
 
@@ -898,11 +1000,34 @@ int mcpt_scene_upload(mcpt_ctx *ctx, const mcpt_triangle *tris, int64_t n_tris, 
       need[k] = best;
     }
     depth4 = std::max(need[0], 1);
-    if (depth4 > 192) return mcpt::fail(MCPT_ERR_LIMIT, "scene_upload: 4-wide stack too deep");
   } else {
     dn4.resize(1);
     std::memset(dn4.data(), 0, sizeof(DevNode4));
   }
+  // the EXACT search tree over the reference's own leaves (their boxes as stored)
+  std::vector<mcpt::LeafRef> leaves;
+  leaves.reserve((size_t)n);
+  for (int64_t i = 0; i < n_nodes; ++i) {
+    const mcpt_bvh_node &b = nodes[i];
+    if (b.left != b.right) continue;
+    mcpt::LeafRef L;
+    const float bx[6] = {b.bbmin[0], b.bbmax[0], b.bbmin[1], b.bbmax[1], b.bbmin[2], b.bbmax[2]};
+    std::memcpy(L.box, bx, sizeof(bx));
+    L.tri = b.left;
+    leaves.push_back(L);
+  }
+  std::vector<mcpt::Node4Rec> near;
+  int32_t depth_near = 1;
+  if (n_int > 0) {
+    const unsigned hw = std::thread::hardware_concurrency();
+    if (mcpt::build_sah4(leaves, near, &depth_near, (int)std::min(16u, std::max(1u, hw))) != 0)
+      return mcpt::fail(MCPT_ERR_ARG, "scene_upload: no leaves");
+  } else {
+    near.resize(1);
+    std::memset(near.data(), 0, sizeof(mcpt::Node4Rec));
+  }
+  depth4 = std::max(depth4, depth_near);
+  if (depth4 > 192) return mcpt::fail(MCPT_ERR_LIMIT, "scene_upload: 4-wide stack too deep");
   std::vector<DevTri> dt(n);
   for (int64_t i = 0; i < n; ++i) {
     const mcpt_triangle &t = tris[i];
@@ -924,14 +1049,16 @@ int mcpt_scene_upload(mcpt_ctx *ctx, const mcpt_triangle *tris, int64_t n_tris, 
   HIP_OK(hipSetDevice(ctx->device));
   mcpt_scene *s = new mcpt_scene();
   s->device = ctx->device;
-  if (hipMalloc(&s->nodes4, dn4.size() * sizeof(DevNode4)) != hipSuccess ||
+  if (hipMalloc(&s->near4, near.size() * sizeof(DevNode4)) != hipSuccess ||
+      hipMalloc(&s->nodes4, dn4.size() * sizeof(DevNode4)) != hipSuccess ||
       hipMalloc(&s->nodes, dn.size() * sizeof(DevNode)) != hipSuccess ||
       hipMalloc(&s->tris, dt.size() * sizeof(DevTri)) != hipSuccess ||
       hipMalloc(&s->mats, n_mats * sizeof(mcpt_material)) != hipSuccess) {
     mcpt_scene_destroy(s);
     return mcpt::fail(MCPT_ERR_HIP, "scene_upload: hipMalloc failed");
   }
-  if (hipMemcpy(s->nodes4, dn4.data(), dn4.size() * sizeof(DevNode4), hipMemcpyHostToDevice) != hipSuccess ||
+  if (hipMemcpy(s->near4, near.data(), near.size() * sizeof(DevNode4), hipMemcpyHostToDevice) != hipSuccess ||
+      hipMemcpy(s->nodes4, dn4.data(), dn4.size() * sizeof(DevNode4), hipMemcpyHostToDevice) != hipSuccess ||
       hipMemcpy(s->nodes, dn.data(), dn.size() * sizeof(DevNode), hipMemcpyHostToDevice) != hipSuccess ||
       hipMemcpy(s->tris, dt.data(), dt.size() * sizeof(DevTri), hipMemcpyHostToDevice) != hipSuccess ||
       hipMemcpy(s->mats, mats, n_mats * sizeof(mcpt_material), hipMemcpyHostToDevice) != hipSuccess) {
@@ -946,6 +1073,7 @@ int mcpt_scene_upload(mcpt_ctx *ctx, const mcpt_triangle *tris, int64_t n_tris, 
   SceneView &v = s->view;
   v.nodes = s->nodes;
   v.nodes4 = s->nodes4;
+  v.near4 = s->near4;
   v.tris = s->tris;
   v.mats = s->mats;
   v.root_min = (f4){root.bbmin[0], root.bbmin[1], root.bbmin[2], root.bbmin[3]};
@@ -962,6 +1090,7 @@ int mcpt_scene_destroy(mcpt_scene *s) {
   (void)hipSetDevice(s->device);
   if (s->nodes) (void)hipFree(s->nodes);
   if (s->nodes4) (void)hipFree(s->nodes4);
+  if (s->near4) (void)hipFree(s->near4);
   if (s->tris) (void)hipFree(s->tris);
   if (s->mats) (void)hipFree(s->mats);
   delete s;
@@ -1081,6 +1210,7 @@ int mcpt_render_frames(mcpt_ctx *ctx, const mcpt_scene *scene, const mcpt_camera
     ctx->last.wave_node_phases = h[4];
     ctx->last.wave_leaf_phases = h[5];
     ctx->last.wave_shade_phases = h[6];
+    ctx->last.order_fallbacks = h[7];
   }
   return MCPT_OK;
 }

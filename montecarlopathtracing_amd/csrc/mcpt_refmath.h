@@ -115,13 +115,46 @@ __device__ inline bool transmit_dir(f4 n, f4 in, float eta_i, float eta_t, f4 &o
   out = cl_normalize((eta * cos_i - cl_sqrt(k)) * n + eta * in);
   return true;
 }
-// randomDirection: shade.cl:40-59 — the angle is formed in double (OpenCL
-// M_PI is a double constant), the radius in float.
+// sin and cos of 0 <= x < 131072, bit-identical to __ocml_sin_f32 /
+// __ocml_cos_f32 there: the gfx9 branch of ocml's __ocmlpriv_trigredsmall_f32
+// (3-term Cody-Waite reduction by pi/2, quadrant = rint(x*2/pi) & 3) and
+// __ocmlpriv_sincosred_f32's two minimax polynomials (its llvm.fmuladd calls
+// are the a*b+c forms below under -ffp-contract=on). ocml selects the
+// Payne-Hanek reduction for |x| >= 131072; randomDirection's angle is always
+// below 2*pi, so keeping that branch out of the kernel drops its 64-bit
+// multiply chain and the registers it holds. Checked exhaustively over all
+// 32768 angles against the ocml calls by mcpt_selfcheck_trig.
+__device__ inline void sincos_small(float x, float &s, float &c) {
+  const float t = __builtin_rintf(x * 0x1.45f306p-1f);
+  float r = __builtin_fmaf(t, -0x1.921fb4p+0f, x);
+  r = __builtin_fmaf(t, -0x1.4442d0p-24f, r);
+  r = __builtin_fmaf(t, -0x1.846988p-48f, r);
+  const int q = (int)t & 3;
+  const float r2 = r * r;
+  float p = r2 * -0x1.983304p-13f + 0x1.110388p-7f;
+  p = r2 * p + -0x1.55553ap-3f;
+  const float sr = r * (r2 * p) + r;
+  float k = r2 * 0x1.aea668p-16f + -0x1.6c9e76p-10f;
+  k = r2 * k + 0x1.5557eep-5f;
+  k = r2 * k + -0x1.000008p-1f;
+  const float cr = r2 * k + 1.0f;
+  const uint32_t flip = q > 1 ? 0x80000000u : 0u;
+  s = __builtin_bit_cast(float, __builtin_bit_cast(uint32_t, (q & 1) ? cr : sr) ^ flip);
+  c = __builtin_bit_cast(float, __builtin_bit_cast(uint32_t, (q & 1) ? -sr : cr) ^ flip);
+}
+// randomDirection's angle for a 15-bit draw: formed in double (OpenCL M_PI
+// is a double constant), then rounded to float (shade.cl:40-59).
+__device__ inline float random_phi(uint32_t r) { return (float)(2 * kClPi / 32768 * (double)r); }
+
+// randomDirection: shade.cl:40-59 — the angle is formed in double, the radius
+// in float.
 __device__ inline f4 random_dir(f4 n, uint32_t &seed) {
   n.w = 0;
-  float phi = (float)(2 * kClPi / 32768 * (double)lcg15(seed));
+  float phi = random_phi(lcg15(seed));
   float u = lcg15(seed) * 1.0f / 32768;
   float s = cl_sqrt(u);
+  float sin_phi, cos_phi;
+  sincos_small(phi, sin_phi, cos_phi);
   f4 a1, a2;
   if (n.z == 0) {
     a1 = (f4){0, 0, 1.0f, 0};
@@ -130,7 +163,7 @@ __device__ inline f4 random_dir(f4 n, uint32_t &seed) {
   }
   a2 = cl_normalize(cl_cross(a1, n));
   a1 = cl_normalize(cl_cross(a2, n));
-  return cl_normalize(cl_cos(phi) * s * a1 + cl_sin(phi) * s * a2 + (1 - u) * n);
+  return cl_normalize(cos_phi * s * a1 + sin_phi * s * a2 + (1 - u) * n);
 }
 // calcFresnel: shade.cl:69-73 (Schlick on the transmitted direction)
 __device__ inline float fresnel(f4 n, f4 d, float ior) {

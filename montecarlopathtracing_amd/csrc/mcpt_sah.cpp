@@ -1,0 +1,213 @@
+// Binned-SAH search tree for the EXACT path (see mcpt_bvh4.h).
+//
+// The reference searches its HLBVH (Morton-order median splits) left-first;
+// the EXACT kernels search this tree nearest-first instead and prove, per
+// ray, that the order cannot change the reference's answer (falling back to
+// the reference tree when it could).  Only the search cost depends on this
+// tree, so it is built for that: surface-area-heuristic splits over 32
+// centroid bins per axis, one reference leaf per slot.
+#include <algorithm>
+#include <cfloat>
+#include <cmath>
+#include <cstring>
+#include <thread>
+
+#include "mcpt_bvh4.h"
+
+namespace mcpt {
+namespace {
+
+struct BinNode {
+  float box[6];
+  int32_t left, right;  // children (binary node ids); -1 for a leaf
+  int32_t item;         // leaf: index into the leaf list
+};
+
+struct Builder {
+  const std::vector<LeafRef> &L;
+  std::vector<float> cen;  // 3 per leaf
+  std::vector<int32_t> idx;
+  std::vector<BinNode> nodes;  // 2m-1, subtree of [lo,hi) at [base, base + 2(hi-lo)-1)
+  int max_threads;
+
+  explicit Builder(const std::vector<LeafRef> &l) : L(l) {}
+
+  static void grow(float *b, const float *x) {
+    for (int a = 0; a < 3; ++a) {
+      b[2 * a] = std::min(b[2 * a], x[2 * a]);
+      b[2 * a + 1] = std::max(b[2 * a + 1], x[2 * a + 1]);
+    }
+  }
+  static void empty(float *b) {
+    for (int a = 0; a < 3; ++a) b[2 * a] = FLT_MAX, b[2 * a + 1] = -FLT_MAX;
+  }
+  static double area(const float *b) {
+    double dx = (double)b[1] - b[0], dy = (double)b[3] - b[2], dz = (double)b[5] - b[4];
+    if (dx < 0) return 0.0;
+    return 2.0 * (dx * dy + dy * dz + dz * dx);
+  }
+
+  // returns the split position in idx (lo < mid < hi)
+  int64_t split(int64_t lo, int64_t hi) {
+    constexpr int NB = 32;
+    float cmin[3] = {FLT_MAX, FLT_MAX, FLT_MAX}, cmax[3] = {-FLT_MAX, -FLT_MAX, -FLT_MAX};
+    for (int64_t i = lo; i < hi; ++i) {
+      const float *c = &cen[3 * (size_t)idx[i]];
+      for (int a = 0; a < 3; ++a) cmin[a] = std::min(cmin[a], c[a]), cmax[a] = std::max(cmax[a], c[a]);
+    }
+    double best = DBL_MAX;
+    int best_axis = -1, best_bin = -1;
+    for (int a = 0; a < 3; ++a) {
+      const float ext = cmax[a] - cmin[a];
+      if (!(ext > 0)) continue;
+      const float scale = NB / ext;
+      float bb[NB][6];
+      int64_t bc[NB];
+      for (int k = 0; k < NB; ++k) empty(bb[k]), bc[k] = 0;
+      for (int64_t i = lo; i < hi; ++i) {
+        const int32_t it = idx[i];
+        int k = std::min(NB - 1, (int)((cen[3 * (size_t)it + a] - cmin[a]) * scale));
+        grow(bb[k], L[it].box);
+        ++bc[k];
+      }
+      double left_cost[NB];
+      float acc[6];
+      empty(acc);
+      int64_t cnt = 0;
+      for (int k = 0; k < NB - 1; ++k) {
+        grow(acc, bb[k]);
+        cnt += bc[k];
+        left_cost[k] = cnt ? area(acc) * (double)cnt : -1.0;
+      }
+      empty(acc);
+      cnt = 0;
+      for (int k = NB - 1; k > 0; --k) {
+        grow(acc, bb[k]);
+        cnt += bc[k];
+        if (!cnt || left_cost[k - 1] < 0) continue;
+        const double c = left_cost[k - 1] + area(acc) * (double)cnt;
+        if (c < best) best = c, best_axis = a, best_bin = k;
+      }
+    }
+    int64_t mid = (lo + hi) / 2;
+    if (best_axis >= 0) {
+      const int a = best_axis;
+      const float scale = NB / (cmax[a] - cmin[a]);
+      auto it = std::stable_partition(idx.begin() + lo, idx.begin() + hi, [&](int32_t t) {
+        return std::min(NB - 1, (int)((cen[3 * (size_t)t + a] - cmin[a]) * scale)) < best_bin;
+      });
+      const int64_t m = it - idx.begin();
+      if (m > lo && m < hi) mid = m;
+    }
+    return mid;
+  }
+
+  void build(int64_t lo, int64_t hi, int64_t base, int depth) {
+    BinNode &n = nodes[base];
+    if (hi - lo == 1) {
+      std::memcpy(n.box, L[idx[lo]].box, sizeof(n.box));
+      n.left = n.right = -1;
+      n.item = idx[lo];
+      return;
+    }
+    const int64_t mid = split(lo, hi);
+    const int64_t lbase = base + 1, rbase = base + 2 * (mid - lo);
+    // the two halves touch disjoint idx ranges and node ranges: safe to run in parallel
+    if ((1 << (depth + 1)) <= max_threads && hi - lo > 65536) {
+      std::thread t([&] { build(lo, mid, lbase, depth + 1); });
+      build(mid, hi, rbase, depth + 1);
+      t.join();
+    } else {
+      build(lo, mid, lbase, depth + 1);
+      build(mid, hi, rbase, depth + 1);
+    }
+    n.left = (int32_t)lbase;
+    n.right = (int32_t)rbase;
+    n.item = -1;
+    std::memcpy(n.box, nodes[lbase].box, sizeof(n.box));
+    grow(n.box, nodes[rbase].box);
+  }
+};
+
+}  // namespace
+
+int build_sah4(const std::vector<LeafRef> &leaves, std::vector<Node4Rec> &out, int32_t *stack_need, int threads) {
+  const int64_t m = (int64_t)leaves.size();
+  out.clear();
+  *stack_need = 1;
+  if (m <= 0) return -1;
+  Builder B(leaves);
+  B.max_threads = std::max(1, threads);
+  B.cen.resize(3 * (size_t)m);
+  B.idx.resize((size_t)m);
+  for (int64_t i = 0; i < m; ++i) {
+    for (int a = 0; a < 3; ++a) B.cen[3 * i + a] = 0.5f * (leaves[i].box[2 * a] + leaves[i].box[2 * a + 1]);
+    B.idx[i] = (int32_t)i;
+  }
+  B.nodes.resize(2 * (size_t)m - 1);
+  B.build(0, m, 0, 0);
+  if (m == 1) return 0;  // a single leaf: the kernels handle it without a node
+
+  // collapse: open the largest-area internal child until 4 slots, keeping
+  // left-to-right order; emit nodes in depth-first preorder
+  const std::vector<BinNode> &N = B.nodes;
+  struct Pending {
+    int32_t bin, out;
+  };
+  std::vector<Pending> todo(1, Pending{0, 0});
+  out.emplace_back();
+  while (!todo.empty()) {
+    const Pending p = todo.back();
+    todo.pop_back();
+    int32_t kids[4] = {N[p.bin].left, N[p.bin].right, -1, -1};
+    int nk = 2;
+    while (nk < 4) {
+      int bi = -1;
+      double ba = -1.0;
+      for (int k = 0; k < nk; ++k)
+        if (N[kids[k]].item < 0 && Builder::area(N[kids[k]].box) > ba) ba = Builder::area(N[kids[k]].box), bi = k;
+      if (bi < 0) break;
+      const int32_t x = kids[bi];
+      for (int k = nk; k > bi + 1; --k) kids[k] = kids[k - 1];
+      kids[bi] = N[x].left;
+      kids[bi + 1] = N[x].right;
+      ++nk;
+    }
+    Node4Rec rec;
+    std::memset(&rec, 0, sizeof(rec));
+    int32_t child_out[4] = {-1, -1, -1, -1};
+    for (int k = 0; k < 4; ++k) {
+      if (k >= nk) {
+        rec.link[k] = kEmptySlot4;
+        continue;
+      }
+      const BinNode &c = N[kids[k]];
+      std::memcpy(rec.q + 6 * k, c.box, sizeof(c.box));
+      if (c.item >= 0) {
+        rec.link[k] = ~leaves[c.item].tri;
+      } else {
+        child_out[k] = (int32_t)out.size();
+        rec.link[k] = child_out[k];
+        out.emplace_back();
+      }
+    }
+    out[p.out] = rec;
+    for (int k = nk - 1; k >= 0; --k)  // preorder: slot 0's subtree next
+      if (child_out[k] >= 0) todo.push_back(Pending{kids[k], child_out[k]});
+  }
+  // children are allocated when their parent is emitted: ids only grow down the tree
+  std::vector<int32_t> need(out.size(), 0);
+  for (int64_t k = (int64_t)out.size() - 1; k >= 0; --k) {
+    int ns = 0, below = 0;
+    for (int s = 0; s < 4; ++s) {
+      if (out[k].link[s] == kEmptySlot4) continue;
+      ++ns;
+      if (out[k].link[s] >= 0) below = std::max(below, need[out[k].link[s]]);
+    }
+    need[k] = ns - 1 + below;
+  }
+  *stack_need = std::max(need[0], 1);
+  return 0;
+}
+
+}  // namespace mcpt

@@ -117,6 +117,13 @@ class Renderer:
         L.check(L.lib().mcpt_get_stats(self.ctx, ctypes.byref(s)))
         return {f: getattr(s, f) for f, _ in L.Stats._fields_ if f != "pad"}
 
+    def selfcheck_trig(self):
+        """(angle, range) mismatch counts of the inline randomDirection sin/cos
+        against the ocml calls (mcpt_selfcheck_trig); (0, 0) on a good build."""
+        a, b = ctypes.c_int64(), ctypes.c_int64()
+        L.check(L.lib().mcpt_selfcheck_trig(self.ctx, ctypes.byref(a), ctypes.byref(b)))
+        return a.value, b.value
+
     def new_state(self, width, height, seeds=None):
         if seeds is None:
             seeds = default_seeds(width * height)

@@ -348,8 +348,11 @@ static int box_test(const float *bmin, const float *bmax, f4 o, f4 d, float tmin
 }
 
 /* intersectObjects, objdef.h:240-275: exhaustive left-first DFS, stack[64] */
+static trace_t traverse_nearest(const mcpt_triangle *tris, const mcpt_bvh_node *nodes, f4 o, f4 d, float tmin);
+
 static trace_t traverse(const mcpt_triangle *tris, const mcpt_bvh_node *nodes, f4 o, f4 d, float tmin) {
   trace_t tr = {FLT_MAX, -1, -1, 0, 0};
+  if (g_prune == 2) return traverse_nearest(tris, nodes, o, d, tmin);
   int32_t stack[64];
   int sp = 1;
   stack[0] = 0;
@@ -377,6 +380,49 @@ static trace_t traverse(const mcpt_triangle *tris, const mcpt_bvh_node *nodes, f
       stack[sp++] = N->right;
       cur = N->left;
     }
+  }
+  return tr;
+}
+
+/* Counting mode 2 only (not the reference's order): nearest-child-first
+ * traversal with t-pruning, the box-test / triangle-test counts an
+ * order-free closest-hit search would need. Same box-test unit as the
+ * DFS above (one test per node entered). */
+static trace_t traverse_nearest(const mcpt_triangle *tris, const mcpt_bvh_node *nodes, f4 o, f4 d, float tmin) {
+  trace_t tr = {FLT_MAX, -1, -1, 0, 0};
+  int32_t stack[64];
+  float stack_t[64];
+  int sp = 0;
+  float tn0;
+  tr.nodes++;
+  if (!box_test(nodes[0].bbmin, nodes[0].bbmax, o, d, tmin, &tn0)) return tr;
+  int32_t cur = 0;
+  for (;;) {
+    const mcpt_bvh_node *N = &nodes[cur];
+    if (N->left == N->right) {
+      float t;
+      tr.tests++;
+      if (tri_test(&tris[N->left], o, d, tmin, &t) && t < tr.t) tr.t = t, tr.tri = N->left, tr.last = N->left;
+      cur = -1;
+    } else {
+      float tl, tq;
+      tr.nodes += 2;
+      int hl = box_test(nodes[N->left].bbmin, nodes[N->left].bbmax, o, d, tmin, &tl) && !(tl > tr.t);
+      int hr = box_test(nodes[N->right].bbmin, nodes[N->right].bbmax, o, d, tmin, &tq) && !(tq > tr.t);
+      if (hl && hr) {
+        int near_left = tl <= tq;
+        stack[sp] = near_left ? N->right : N->left;
+        stack_t[sp++] = near_left ? tq : tl;
+        cur = near_left ? N->left : N->right;
+      } else {
+        cur = hl ? N->left : (hr ? N->right : -1);
+      }
+    }
+    while (cur < 0 && sp > 0) {
+      --sp;
+      if (!(stack_t[sp] > tr.t)) cur = stack[sp];
+    }
+    if (cur < 0) break;
   }
   return tr;
 }

@@ -77,7 +77,7 @@ def render(data, cam, w, h, max_depth, frames, max_attempt, seeds, frame_begin=0
     hist = np.zeros((w * h, 4), np.float32) if hist is None else hist.copy()
     count = np.zeros(w * h, np.int32) if count is None else count.copy()
     stats = np.zeros(4, np.uint64)
-    so().oracle_set_prune(int(bool(prune)))
+    so().oracle_set_prune(int(prune))
     if pixels is None:
         so().oracle_render(P(cam), P(data.tris), P(data.nodes), P(data.mats), i32(w), i32(h), i32(max_depth),
                            i32(frame_begin), i32(frames), i32(max_attempt), P(seeds), P(hist), P(count), i32(threads),

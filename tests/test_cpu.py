@@ -281,3 +281,25 @@ def test_oracle_image_vs_reference(name, getter, cam, stride):
     assert (cnt[px] == g["count"][px]).mean() >= 0.97
     rel = np.abs(mh[:, :3].mean(0) - rh[:, :3].mean(0)) / rh[:, :3].mean(0)
     assert (rel < 0.01).all(), rel
+
+
+@pytest.fixture(scope="module")
+def sah_check_exe(tmp_path_factory):
+    import subprocess
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    csrc = os.path.join(root, "montecarlopathtracing_amd", "csrc")
+    exe = str(tmp_path_factory.mktemp("sah") / "sah_check")
+    subprocess.run(["g++", "-O2", "-std=c++17", "-pthread", "-I", csrc, os.path.join(root, "tests", "native", "sah_check.cpp"),
+                    os.path.join(csrc, "mcpt_sah.cpp"), "-o", exe], check=True)
+    return exe
+
+
+@pytest.mark.parametrize("n,seed,clustered", [(1, 1, 0), (2, 1, 0), (5, 3, 1), (1000, 2, 1), (200000, 4, 0)])
+def test_sah_search_tree_invariants(sah_check_exe, n, seed, clustered):
+    """The EXACT path's SAH tree (csrc/mcpt_sah.cpp): every reference leaf
+    exactly once with its own box, every slot box the exact union of its
+    child's, children after parents, the stack bound, and the same bytes for 1
+    or 8 build threads (tests/native/sah_check.cpp)."""
+    import subprocess
+    out = subprocess.run([sah_check_exe, str(n), str(seed), str(clustered)], capture_output=True, text=True, timeout=120)
+    assert out.returncode == 0 and out.stdout.startswith("ok"), out.stdout + out.stderr

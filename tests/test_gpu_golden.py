@@ -31,6 +31,11 @@ def rnd():
     return R.Renderer(0)
 
 
+def test_inline_sincos_matches_ocml(rnd):
+    # all 32768 randomDirection angles and every float in [0, 8), bit for bit
+    assert rnd.selfcheck_trig() == (0, 0)
+
+
 @pytest.mark.parametrize("k", list(CAMS))
 def test_rays_equal_golden(rnd, k):
     mine = R.records(rnd.generate_rays(S.parse_camera(CAMS[k]), 64, 48), L.RAY)

@@ -149,6 +149,28 @@ def test_render_frames_bitexact(rnd, name, getter, camjson, depth):
     assert_bits_equal(h_, rh, "hist")
 
 
+NEAR_TIES = [("cbox", 0.0, scenes.CBOX_CAM), ("mis", 0.0, scenes.MIS_CAM), ("mis", 3e-6, scenes.MIS_CAM)]
+
+
+@needs_ref
+@pytest.mark.parametrize("name,offset,camjson", NEAR_TIES)
+def test_near_ties_bitexact(rnd, name, offset, camjson):
+    """Twin triangles less than EPS apart: the nearest-first search must hand
+    these rays to the reference-order search and still match bit for bit."""
+    data = scenes.near_ties(name, offset)
+    _bounce_chain(rnd, data, camjson, 48, 40, 4, L.MODE_EXACT)
+    rnd.set_stats(True)
+    try:
+        (h_, c_, s_), (rh, rc, rs) = _render_both(rnd, data, camjson, 64, 64, 6, 4, 4)
+        fallbacks = rnd.stats()["order_fallbacks"]
+    finally:
+        rnd.set_stats(False)
+    assert_bits_equal(c_, rc, "count")
+    assert_bits_equal(s_, rs, "seeds")
+    assert_bits_equal(h_, rh, "hist")
+    assert fallbacks > 0
+
+
 @needs_ref
 def test_render_frames_chunked_and_striped_bitexact(rnd):
     """Frames split across launches and rows split into stripes (the multi-GPU

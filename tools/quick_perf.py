@@ -39,9 +39,10 @@ def main():
                 mode, stats, frames, dt, nominal, s["kernel_ms"], s["launches"]))
             if stats:
                 seg = s["segments"]
-                print("   segments %.3g (%.2f/path) nodes/seg %.2f tris/seg %.2f bad %d active Mseg/s %.1f" % (
-                    seg, seg / (w * h * frames), s["node_visits"] / seg, s["tri_tests"] / seg, s["bad_material"],
-                    seg / dt / 1e6))
+                print("   segments %.3g (%.2f/path) nodes/seg %.2f tris/seg %.2f bad %d order fallbacks %d "
+                      "active Mseg/s %.1f" % (seg, seg / (w * h * frames), s["node_visits"] / seg,
+                                              s["tri_tests"] / seg, s["bad_material"], s["order_fallbacks"],
+                                              seg / dt / 1e6))
                 if s["wave_node_phases"]:
                     print("   SIMT: node %.3f leaf %.3f shade %.3f (lanes active per phase / 64)" % (
                         s["node_visits"] / (64.0 * s["wave_node_phases"]),
