@@ -100,10 +100,11 @@ def cpu_baseline(data, cam, h_img, target_s=15.0):
     seeds = default_seeds(W * h_img)
     stride = 61
     px = np.arange(0, W * h_img, stride, dtype=np.int32)
+    O.render(data, cam, W, h_img, DEPTH, 1, 1 << 20, seeds, pixels=px[:2048], threads=threads)  # warm
     t0 = time.time()
-    O.render(data, cam, W, h_img, DEPTH, 1, 1 << 20, seeds, pixels=px[:2048], threads=threads)
-    probe = max(time.time() - t0, 1e-3)
-    frames = int(max(1, min(4096, target_s / (probe * len(px) / 2048.0))))
+    O.render(data, cam, W, h_img, DEPTH, 8, 1 << 20, seeds, pixels=px, threads=threads)
+    probe = max(time.time() - t0, 1e-3) / 8.0  # seconds per frame of the sample
+    frames = int(max(1, min(4096, target_s / probe)))
     t0 = time.time()
     _, _, _, st = O.render(data, cam, W, h_img, DEPTH, frames, 1 << 20, seeds, pixels=px, threads=threads)
     dt = time.time() - t0
@@ -209,6 +210,15 @@ def main():
                     "kernel": "k_render<0,false>",
                     "kernel_node_fetches_per_seg": round(cst["node_visits"] / max(segments, 1), 3),
                     "kernel_tri_tests_per_seg": round(cst["tri_tests"] / max(segments, 1), 3)}
+            # the records this kernel itself gathers per segment (128-B 4-wide
+            # nodes, 64-B triangles, 48 B of pixel state per pixel-launch):
+            # frac > 1 above means the kernel needs fewer bytes than the
+            # reference traversal's B_seg, not that it beats HBM
+            own = (128.0 * cst["node_visits"] + 64.0 * cst["tri_tests"]
+                   + 48.0 * W * H_PER_GPU * max(cst["launches"], 1)) / max(segments, 1)
+            roof["own_bytes_per_seg"] = round(own, 1)
+            roof["own_achieved"] = round(own * seg_per_launch / avg_launch_s / 1e9, 1)
+            roof["own_frac"] = round(roof["own_achieved"] / HBM_PEAK_GBS, 4)
         cpu = None
         if n == 1 and not args.no_cpu and args.workload == "C2":
             cpu = cpu_baseline(data, cam, h_img)

@@ -121,7 +121,8 @@ typedef struct mcpt_render_params {
   int32_t stripe_index;             /* this GPU's stripe residue            */
   int32_t stripe_count;             /* number of GPUs (1 = whole image)     */
   int32_t mode;                     /* MCPT_MODE_*                          */
-  int32_t frames_per_launch;        /* 0 = auto                             */
+  int32_t frames_per_launch;        /* frames per block (a lane runs one pixel
+                                       for one block, then hands it on); 0 = 16 */
   int32_t reserved;
 } mcpt_render_params;
 

@@ -111,8 +111,10 @@ struct mcpt_ctx {
   int device;
   bool stats_on = false;
   unsigned long long *d_stats = nullptr;  // segments, nodes, tris, bad, wave T/L/S phases
-  int32_t *d_queue = nullptr;             // k_render work-queue heads, one per launch
+  uint32_t *d_queue = nullptr;            // k_render work-queue heads, one per launch
   int32_t queue_cap = 0;
+  int32_t *d_progress = nullptr;          // k_render per-pixel block progress
+  int64_t progress_cap = 0;
   int32_t resident_blocks[2] = {0, 0};   // occupancy of k_render<EXACT|NOPRUNE> (64-thread blocks/CU)
   mcpt_stats last;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
@@ -486,6 +488,16 @@ __device__ inline f4 accumulate_one(f4 now, f4 &hist, int32_t &cnt, int max_atte
 }
 
 // --------------------------------------------------------- fused hot kernel
+// Accesses that hand a pixel's state from one lane to another inside a launch.
+// They bypass the per-CU and per-XCD caches (sc0 sc1), so they meet in memory
+// whichever XCDs the two lanes run on.
+__device__ inline int32_t sys_load(const int32_t *p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ inline void sys_store(int32_t *p, int32_t v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 struct RenderArgs {
   mcpt_camera cam;
   SceneView S;
@@ -495,11 +507,14 @@ struct RenderArgs {
   unsigned long long *stats;
   int32_t W, H, local_rows, tiles_x;
   int32_t stripe_rows, stripe_index, stripe_count;
-  int32_t max_depth, max_attempt, frame_begin, frames;
+  int32_t max_depth, max_attempt, frame_begin, frames;  // frames: of this launch
+  int32_t fpl, blocks;         // frames per block, blocks in this launch
+  int32_t *progress;           // per pixel: blocks published in this launch
   int32_t stack_depth;
   int32_t th_leaf, th_shade;  // lanes waiting before the L / S phase runs
-  int32_t *queue;             // pixel work-queue head (zeroed before each launch)
+  uint32_t *queue;            // work-queue head (zeroed before each launch)
   int32_t lds_mats;           // 1: copy the material table to LDS after the stack
+  int32_t chunk;              // queue entries a wave claims per atomic (at least)
 };
 
 __device__ inline int32_t global_row(int32_t lr, const RenderArgs &A) {
@@ -583,39 +598,79 @@ __global__ void __launch_bounds__(64, MCPT_WAVES_PER_SIMD) k_render(RenderArgs A
     else
       cur = kDone;
   };
-  const int32_t n_items = A.tiles_x * ((A.local_rows + 7) >> 3) * 64;
+  // queue entry q = block * n_items + item: frame block q / n_items of pixel
+  // slot q % n_items (8x8 tiles).  Blocks of one pixel run in order: the
+  // lane that takes (p, b > 0) waits until the lane that ran (p, b - 1)
+  // has published its state (A.progress[p] = b).
+  const uint32_t n_items = (uint32_t)A.tiles_x * (uint32_t)((A.local_rows + 7) >> 3) * 64u;
+  const uint32_t n_total = n_items * (uint32_t)A.blocks;
+  uint32_t pool = 0, pool_left = 0;  // wave-uniform: claimed, not yet started queue entries
+  bool pending = false;              // holds entry pq, not started yet
+  uint32_t pq = 0;
+  int32_t blk = 0;
 
   for (;;) {
-    // ---- fetch: lanes without a pixel take the next queue entries (one atomic per wave)
+    // ---- fetch: lanes without work take the next queue entries, from the
+    // wave's pool of claimed entries; one atomic claims max(chunk, shortfall)
     {
-      const bool need = alive && !has_px;
+      const bool need = alive && !has_px && !pending;
       const unsigned long long mn = __ballot(need);
       if (mn) {
-        const int leader = __builtin_ctzll(mn);
-        int32_t base = 0;
-        if (lane == leader) base = atomicAdd(A.queue, __popcll(mn));
-        base = __shfl(base, leader);
+        const uint32_t n_need = (uint32_t)__popcll(mn);
+        const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(mn >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mn, 0));
+        uint32_t q = pool + rank;
+        if (n_need <= pool_left) {
+          pool += n_need;
+          pool_left -= n_need;
+        } else {
+          const uint32_t claim = max((uint32_t)A.chunk, n_need - pool_left);
+          const int leader = __builtin_ctzll(mn);
+          uint32_t base = 0;
+          if (lane == leader) base = atomicAdd(A.queue, claim);
+          base = __builtin_amdgcn_readfirstlane(__shfl(base, leader));
+          if (rank >= pool_left) q = base + (rank - pool_left);
+          pool = base + (n_need - pool_left);
+          pool_left = claim - (n_need - pool_left);
+        }
         if (need) {
-          const int32_t q = base + (int32_t)__builtin_amdgcn_mbcnt_hi((uint32_t)(mn >> 32),
-                                                                       __builtin_amdgcn_mbcnt_lo((uint32_t)mn, 0));
-          if (q >= n_items) {
+          if (q >= n_total) {
             alive = false;
           } else {
-            const int32_t tile = q >> 6, k = q & 63;
-            const int32_t x = (tile % A.tiles_x) * 8 + (k & 7);
-            const int32_t lr = (tile / A.tiles_x) * 8 + (k >> 3);
-            const int32_t y = lr < A.local_rows ? global_row(lr, A) : A.H;
-            if (x < A.W && y < A.H) {  // else: an edge-tile hole, fetch again
-              has_px = true;
-              pid = y * A.W + x;
-              seed = A.seeds[pid];
-              hist = A.hist[pid];
-              cnt = A.count[pid];
-              f = 0;
-              pxy = (uint32_t)x | ((uint32_t)y << 16);
-              primary();
-              begin_segment();
-            }
+            pending = true;
+            pq = q;
+          }
+        }
+      }
+      if (pending) {  // start the entry once its pixel's previous block is published
+        const uint32_t b = pq / n_items, it = pq - b * n_items;
+        const int32_t tile = (int32_t)(it >> 6), k = (int32_t)(it & 63);
+        const int32_t x = (tile % A.tiles_x) * 8 + (k & 7);
+        const int32_t lr = (tile / A.tiles_x) * 8 + (k >> 3);
+        const int32_t y = lr < A.local_rows ? global_row(lr, A) : A.H;
+        if (x >= A.W || y >= A.H) {  // an edge-tile hole: fetch again
+          pending = false;
+        } else {
+          const int32_t p = y * A.W + x;
+          if (b == 0) {  // state from before this launch
+            pending = false;
+            seed = A.seeds[p];
+            hist = A.hist[p];
+            cnt = A.count[p];
+          } else if (sys_load(&A.progress[p]) >= (int32_t)b) {  // published by another lane, any XCD
+            pending = false;
+            seed = (uint32_t)sys_load((const int32_t *)&A.seeds[p]);
+            const int32_t *hp = (const int32_t *)&A.hist[p];
+            hist = (f4){as_f(sys_load(hp)), as_f(sys_load(hp + 1)), as_f(sys_load(hp + 2)), as_f(sys_load(hp + 3))};
+            cnt = sys_load(&A.count[p]);
+          }
+          if (!pending) {
+            has_px = true;
+            blk = (int32_t)b;
+            pid = p;
+            f = 0;
+            pxy = (uint32_t)x | ((uint32_t)y << 16);
+            primary();
+            begin_segment();
           }
         }
       }
@@ -707,13 +762,27 @@ __global__ void __launch_bounds__(64, MCPT_WAVES_PER_SIMD) k_render(RenderArgs A
         }
         if (done) {
           // ColorOut: history runs while attemptCount <= MAX_ATTEMPT (colorout.cpp:56)
-          if (A.frame_begin + f <= A.max_attempt) (void)accumulate_one(color, hist, cnt, A.max_attempt);
+          const int32_t f0 = blk * A.fpl;
+          if (A.frame_begin + f0 + f <= A.max_attempt) (void)accumulate_one(color, hist, cnt, A.max_attempt);
           ++f;
-          if (f < A.frames) primary();
-          if (f == A.frames) {  // pixel complete: write back, fetch another next iteration
-            A.seeds[pid] = seed;
-            A.hist[pid] = hist;
-            A.count[pid] = cnt;
+          const int32_t fend = min(A.fpl, A.frames - f0);
+          if (f < fend) primary();
+          if (f == fend) {  // block complete: write back, fetch another next iteration
+            if (blk + 1 < A.blocks) {  // publish for the lane that takes the next block
+              sys_store((int32_t *)&A.seeds[pid], (int32_t)seed);
+              int32_t *hp = (int32_t *)&A.hist[pid];
+              sys_store(hp, as_i(hist.x));
+              sys_store(hp + 1, as_i(hist.y));
+              sys_store(hp + 2, as_i(hist.z));
+              sys_store(hp + 3, as_i(hist.w));
+              sys_store(&A.count[pid], cnt);
+              asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // state reaches memory before the flag
+              sys_store(&A.progress[pid], blk + 1);
+            } else {
+              A.seeds[pid] = seed;
+              A.hist[pid] = hist;
+              A.count[pid] = cnt;
+            }
             has_px = false;
           }
         }
@@ -857,6 +926,7 @@ int mcpt_ctx_destroy(mcpt_ctx *c) {
   (void)hipSetDevice(c->device);
   if (c->d_stats) (void)hipFree(c->d_stats);
   if (c->d_queue) (void)hipFree(c->d_queue);
+  if (c->d_progress) (void)hipFree(c->d_progress);
   if (c->ev0) (void)hipEventDestroy(c->ev0);
   if (c->ev1) (void)hipEventDestroy(c->ev1);
   delete c;
@@ -1135,30 +1205,45 @@ int mcpt_render_frames(mcpt_ctx *ctx, const mcpt_scene *scene, const mcpt_camera
   A.max_depth = p->max_depth;
   A.max_attempt = p->max_attempt;
   A.stack_depth = scene->stack_depth;
-  A.th_leaf = 8;
-  A.th_shade = 16;
+  A.th_leaf = 4;  // tuned on C2 (tools/sweep_env.sh): leaf phase at >= 4 lanes, shade at >= 32
+  A.th_shade = 32;
   if (const char *e = std::getenv("MCPT_PHASE_THRESHOLDS")) {  // tuning knob: "leaf,shade"
     int a = 0, b = 0;
     if (std::sscanf(e, "%d,%d", &a, &b) == 2 && a >= 1 && b >= 1) A.th_leaf = a, A.th_shade = b;
   }
+  A.chunk = 4;  // one queue atomic per >= 4 entries: the single counter's atomic rate binds below that
+  if (const char *e = std::getenv("MCPT_QUEUE_CHUNK")) A.chunk = std::max(1, std::min(4096, std::atoi(e)));  // tuning knob
   const int64_t tiles = (int64_t)A.tiles_x * ((A.local_rows + 7) / 8);
   const int depth_entries = p->mode == MCPT_MODE_NOPRUNE ? scene->stack_depth : scene->stack_depth4;
   A.stack_depth = depth_entries;
   A.lds_mats = scene->n_mats <= 256 ? 1 : 0;
   const size_t lds = (size_t)depth_entries * 64 * sizeof(int32_t) + (A.lds_mats ? scene->n_mats * sizeof(mcpt_material) : 0);
-  int fpl = p->frames_per_launch;
-  if (fpl <= 0) {  // aim for ~2^26 lane-frames per launch: long enough to amortise, short enough to stream
-    int64_t px = (int64_t)p->width * A.local_rows;
-    fpl = (int)std::max<int64_t>(1, std::min<int64_t>(p->frames, (int64_t(1) << 26) / std::max<int64_t>(px, 1)));
-  }
-  const int n_launch = (p->frames + fpl - 1) / fpl;
+  // frames_per_launch = frames per BLOCK: a lane runs one pixel for one block
+  // of frames, then hands the pixel's state to whichever lane takes its next
+  // block.  One launch runs many blocks of every pixel, block-major, so lanes
+  // stay busy until the last block (no per-block drain of the GPU).
+  const int fpl = p->frames_per_launch > 0 ? p->frames_per_launch : 16;
+  const uint32_t n_items = (uint32_t)A.tiles_x * (uint32_t)((A.local_rows + 7) / 8) * 64u;
+  const int64_t max_blocks = std::max<int64_t>(1, std::min<int64_t>(INT32_MAX / std::max<uint32_t>(n_items, 1), 4096 / fpl + 1));
+  const int64_t n_blocks_all = (p->frames + fpl - 1) / fpl;
+  const int n_launch = (int)((n_blocks_all + max_blocks - 1) / max_blocks);
   if (n_launch > ctx->queue_cap) {  // one queue head per launch, zeroed by a single memset
     if (ctx->d_queue) HIP_OK(hipFree(ctx->d_queue));
     ctx->d_queue = nullptr;
     ctx->queue_cap = 0;
-    HIP_OK(hipMalloc(&ctx->d_queue, (size_t)std::max(n_launch, 64) * sizeof(int32_t)));
+    HIP_OK(hipMalloc(&ctx->d_queue, (size_t)std::max(n_launch, 64) * sizeof(uint32_t)));
     ctx->queue_cap = std::max(n_launch, 64);
   }
+  const int64_t n_px = (int64_t)p->width * p->height;
+  if (n_blocks_all > 1 && n_px > ctx->progress_cap) {
+    if (ctx->d_progress) HIP_OK(hipFree(ctx->d_progress));
+    ctx->d_progress = nullptr;
+    ctx->progress_cap = 0;
+    HIP_OK(hipMalloc(&ctx->d_progress, (size_t)n_px * sizeof(int32_t)));
+    ctx->progress_cap = n_px;
+  }
+  A.fpl = fpl;
+  A.progress = ctx->d_progress;
   // persistent grid: as many 64-lane workgroups as can be resident at once
   const bool noprune = p->mode == MCPT_MODE_NOPRUNE;
   const void *kfn = noprune ? (ctx->stats_on ? (const void *)k_render<MCPT_MODE_NOPRUNE, true>
@@ -1173,11 +1258,13 @@ int mcpt_render_frames(mcpt_ctx *ctx, const mcpt_scene *scene, const mcpt_camera
   HIP_OK(hipEventRecord(ctx->ev0, st));
   int launches = 0;
   if (tiles > 0 && p->frames > 0) {
-    HIP_OK(hipMemsetAsync(ctx->d_queue, 0, (size_t)n_launch * sizeof(int32_t), st));
-    for (int f0 = 0; f0 < p->frames; f0 += fpl) {
-      A.frame_begin = p->frame_begin + f0;
-      A.frames = std::min(fpl, p->frames - f0);
+    HIP_OK(hipMemsetAsync(ctx->d_queue, 0, (size_t)n_launch * sizeof(uint32_t), st));
+    for (int64_t f0 = 0; f0 < p->frames; f0 += max_blocks * fpl) {
+      A.frame_begin = p->frame_begin + (int32_t)f0;
+      A.frames = (int32_t)std::min<int64_t>(max_blocks * fpl, p->frames - f0);
+      A.blocks = (A.frames + fpl - 1) / fpl;
       A.queue = ctx->d_queue + launches;
+      if (A.blocks > 1) HIP_OK(hipMemsetAsync(ctx->d_progress, 0, (size_t)n_px * sizeof(int32_t), st));
       if (noprune) {
         if (ctx->stats_on)
           hipLaunchKernelGGL((k_render<MCPT_MODE_NOPRUNE, true>), dim3(grid), dim3(64), lds, st, A);

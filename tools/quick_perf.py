@@ -29,14 +29,20 @@ def main():
             st = r.new_state(w, h)
             r.render_frames(dsc, cam, st, depth, 1 << 20, 1, mode=mode)  # warm
             torch.cuda.synchronize()
-            t0 = time.time()
-            r.render_frames(dsc, cam, st, depth, 1 << 20, frames, mode=mode)
-            torch.cuda.synchronize()
-            dt = time.time() - t0
-            s = r.stats()
-            nominal = w * h * frames * depth / dt / 1e6
-            print("mode=%d stats=%d frames=%d %.3fs nominal %.1f Msamples/s kernel_ms=%.1f launches=%d" % (
-                mode, stats, frames, dt, nominal, s["kernel_ms"], s["launches"]))
+            reps = 1 if stats else int(os.environ.get("QP_REPS", "7"))
+            kms = []
+            for _ in range(reps):  # median of reps launches (single launches vary by ~5 %)
+                t0 = time.time()
+                r.render_frames(dsc, cam, st, depth, 1 << 20, frames, mode=mode,
+                                frames_per_launch=int(os.environ.get("QP_FPL", "0")))
+                torch.cuda.synchronize()
+                dt = time.time() - t0
+                s = r.stats()
+                kms.append(s["kernel_ms"])
+            km = sorted(kms)[len(kms) // 2]
+            nominal = w * h * frames * depth / (km / 1e3) / 1e6
+            print("mode=%d stats=%d frames=%d nominal %.1f Msamples/s kernel_ms median %.2f (min %.2f max %.2f, %d reps)"
+                  % (mode, stats, frames, nominal, km, min(kms), max(kms), reps))
             if stats:
                 seg = s["segments"]
                 print("   segments %.3g (%.2f/path) nodes/seg %.2f tris/seg %.2f bad %d order fallbacks %d "
