@@ -116,15 +116,17 @@ def cpu_baseline(data, cam, h_img, target_s=15.0):
             "active_Msegments_per_s": float(st[0]) / dt / 1e6}
 
 
-def load_traffic():
-    """HBM bytes per launch from the committed rocprofv3 PMC summary, if any."""
+def load_traffic(workload, steps):
+    """Memory-side bytes per launch of the hot kernel from the committed
+    rocprofv3 PMC summary (tools/summarize_profiles.py), for this workload
+    and launch size only; None otherwise."""
     path = os.path.join(ROOT, "profiles", "pmc_summary.json")
     try:
         with open(path) as fh:
-            j = json.load(fh)
-        return j.get("hbm_bytes_per_launch")
+            j = json.load(fh).get(workload) or {}
     except (OSError, ValueError):
         return None
+    return j.get("hbm_bytes_per_launch") if j.get("frames_per_launch") == steps else None
 
 
 def main():
@@ -202,7 +204,7 @@ def main():
             seg_per_launch = segments / float(launches)
             avg_launch_s = kernel_ms / 1e3 / launches
             achieved = b_seg * seg_per_launch / avg_launch_s / 1e9
-            traffic = load_traffic()
+            traffic = load_traffic(args.workload, args.steps)
             roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                     "B_seg": round(b_seg, 1), "E_node": round(ec["E_node"], 3), "E_tri": round(ec["E_tri"], 3),
@@ -219,6 +221,11 @@ def main():
             roof["own_bytes_per_seg"] = round(own, 1)
             roof["own_achieved"] = round(own * seg_per_launch / avg_launch_s / 1e9, 1)
             roof["own_frac"] = round(roof["own_achieved"] / HBM_PEAK_GBS, 4)
+            # the measured streaming-read bandwidth beside the spec
+            try:
+                roof["measured_read_peak"] = round(rnd.measure_read_bw(4 << 30), 1)
+            except Exception as e:  # reported, never fatal to the bench line
+                roof["measured_read_peak"] = "unavailable: %s" % e
         cpu = None
         if n == 1 and not args.no_cpu and args.workload == "C2":
             cpu = cpu_baseline(data, cam, h_img)

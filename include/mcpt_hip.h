@@ -230,6 +230,11 @@ int mcpt_accumulate(mcpt_ctx *ctx, float *color_dev, float *hist_dev, int32_t *c
 int mcpt_set_stats(mcpt_ctx *ctx, int32_t enabled);
 int mcpt_get_stats(mcpt_ctx *ctx, mcpt_stats *out);
 
+/* Streaming-read bandwidth of this GPU's HBM (GB/s, best of 5 reads of
+ * `bytes` after a warm-up): the measured roofline denominator SURVEY.md
+ * §8(d) asks for next to the 8 TB/s spec.                                 */
+int mcpt_measure_read_bw(mcpt_ctx *ctx, int64_t bytes, double *gbps);
+
 /* Device self-check of the inline sin/cos used by randomDirection
  * (shade.cl:40-59) against the ocml library calls the reference kernel
  * makes: mismatching bit patterns over the 32768 angles 2*pi*r/32768 and

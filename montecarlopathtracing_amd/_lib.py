@@ -83,6 +83,7 @@ SIGNATURES = {
     "mcpt_set_stats": (_I32, [_P, _I32]),
     "mcpt_get_stats": (_I32, [_P, _P]),
     "mcpt_selfcheck_trig": (_I32, [_P, _P, _P]),
+    "mcpt_measure_read_bw": (_I32, [_P, _I64, _P]),
 }
 
 _lib = None

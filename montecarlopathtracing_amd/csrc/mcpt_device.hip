@@ -961,6 +961,48 @@ int mcpt_selfcheck_trig(mcpt_ctx *c, int64_t *angle_bad, int64_t *range_bad) {
   return MCPT_OK;
 }
 
+// Streaming read of n float4 (grid-stride, 16 B per lane per load), one
+// partial sum per block so nothing is optimised away (mcpt_measure_read_bw).
+__global__ void __launch_bounds__(256) k_stream_read(const f4 *__restrict__ src, int64_t n, float *sink) {
+  f4 acc = (f4){0.0f, 0.0f, 0.0f, 0.0f};
+  const int64_t stride = (int64_t)gridDim.x * 256;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += stride) acc += __builtin_nontemporal_load(&src[i]);
+  const float v = acc.x + acc.y + acc.z + acc.w;
+  if (v == 12345.678f) sink[blockIdx.x] = v;  // never true for the zeroed buffer
+}
+
+int mcpt_measure_read_bw(mcpt_ctx *c, int64_t bytes, double *gbps) {
+  if (!c || !gbps || bytes < (1 << 20)) return mcpt::fail(MCPT_ERR_ARG, "measure_read_bw: bad argument");
+  HIP_OK(hipSetDevice(c->device));
+  const int64_t n = bytes / 16;
+  void *buf = nullptr;
+  float *sink = nullptr;
+  if (hipMalloc(&buf, (size_t)n * 16) != hipSuccess) return mcpt::fail(MCPT_ERR_HIP, "measure_read_bw: hipMalloc");
+  int n_cu = 0;
+  (void)hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, c->device);
+  const int grid = std::max(1, n_cu) * 32;
+  if (hipMalloc(&sink, grid * sizeof(float)) != hipSuccess || hipMemset(buf, 0, (size_t)n * 16) != hipSuccess) {
+    (void)hipFree(buf);
+    if (sink) (void)hipFree(sink);
+    return mcpt::fail(MCPT_ERR_HIP, "measure_read_bw: setup");
+  }
+  float best = 1e30f;
+  for (int rep = 0; rep < 6; ++rep) {
+    (void)hipEventRecord(c->ev0, 0);
+    hipLaunchKernelGGL(k_stream_read, dim3(grid), dim3(256), 0, 0, (const f4 *)buf, n, sink);
+    (void)hipEventRecord(c->ev1, 0);
+    (void)hipEventSynchronize(c->ev1);
+    float ms = 0.0f;
+    (void)hipEventElapsedTime(&ms, c->ev0, c->ev1);
+    if (rep > 0) best = std::min(best, ms);  // rep 0 warms up
+  }
+  (void)hipFree(buf);
+  (void)hipFree(sink);
+  HIP_OK(hipGetLastError());
+  *gbps = (double)n * 16.0 / (best * 1e-3) / 1e9;
+  return MCPT_OK;
+}
+
 int mcpt_set_stats(mcpt_ctx *c, int32_t on) {
   if (!c) return mcpt::fail(MCPT_ERR_ARG, "set_stats: null ctx");
   c->stats_on = on != 0;

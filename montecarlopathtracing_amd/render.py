@@ -124,6 +124,12 @@ class Renderer:
         L.check(L.lib().mcpt_selfcheck_trig(self.ctx, ctypes.byref(a), ctypes.byref(b)))
         return a.value, b.value
 
+    def measure_read_bw(self, nbytes=4 << 30):
+        """Streaming HBM read bandwidth in GB/s (mcpt_measure_read_bw)."""
+        g = ctypes.c_double()
+        L.check(L.lib().mcpt_measure_read_bw(self.ctx, int(nbytes), ctypes.byref(g)))
+        return g.value
+
     def new_state(self, width, height, seeds=None):
         if seeds is None:
             seeds = default_seeds(width * height)

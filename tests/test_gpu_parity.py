@@ -209,3 +209,23 @@ def test_exact_equals_noprune_full_size(rnd):
     for a, b, what in zip(outs[0], outs[1], ("hist", "count", "seeds")):
         assert_bits_equal(a, b, what)
     dsc.close()
+
+
+def test_frame_blocks_handoff_full_size(rnd):
+    """Frame blocks of one pixel run on different lanes (and XCDs) within one
+    launch, handing the state through memory: any block size gives the same
+    bits as one block per pixel."""
+    data, cam = scenes.cbox_diffuse(), S.parse_camera(scenes.CBOX_CAM)
+    w = h = 512
+    seeds = R.default_seeds(w * h)
+    dsc = rnd.upload(data)
+    outs = []
+    for fpl in (24, 1, 5):
+        st = rnd.new_state(w, h, seeds)
+        rnd.render_frames(dsc, cam, st, 8, 1 << 20, 24, frames_per_launch=fpl)
+        torch.cuda.synchronize()
+        outs.append((st.hist.cpu().numpy(), st.count.cpu().numpy(), st.seeds_np()))
+    for o in outs[1:]:
+        for a, b, what in zip(outs[0], o, ("hist", "count", "seeds")):
+            assert_bits_equal(a, b, what)
+    dsc.close()

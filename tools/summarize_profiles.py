@@ -57,8 +57,18 @@ def main():
                    "(raw read bytes = half). Counts include Infinity-Cache hits.",
            "source": ["profiles/%s_pmc_fetch_size.csv" % tag, "profiles/%s_pmc_write_size.csv" % tag,
                       "profiles/%s_bench_kernel_stats.csv" % tag]}
-    with open(os.path.join(dst, "pmc_summary.json"), "w") as fh:
-        json.dump(out, fh, indent=1)
+    out["frames_per_launch"] = bench["steps"]
+    wl = bench["config"]["workload"].split(":")[0]
+    path = os.path.join(dst, "pmc_summary.json")
+    try:
+        allw = json.load(open(path))
+        if "kernel" in allw:  # the old single-workload layout
+            allw = {}
+    except (OSError, ValueError):
+        allw = {}
+    allw[wl] = out
+    with open(path, "w") as fh:
+        json.dump(allw, fh, indent=1)
     print(json.dumps(out, indent=1))
 
 

@@ -1,9 +1,8 @@
-export QP_REPS=5 MCPT_PHASE_THRESHOLDS=4,32
-for fpl in 16 8; do for c in 2 4 8 16 32; do
-  echo "== fpl $fpl chunk $c"
-  QP_FPL=$fpl MCPT_QUEUE_CHUNK=$c timeout -k 10 120 python tools/quick_perf.py 64 1024 2>&1 | grep "stats=0" || exit 1
-done; done
-for t in 2,32 4,24 4,40 8,32; do
-  echo "== fpl 16 chunk 8 th $t"
-  QP_FPL=16 MCPT_QUEUE_CHUNK=8 MCPT_PHASE_THRESHOLDS=$t timeout -k 10 120 python tools/quick_perf.py 64 1024 2>&1 | grep "stats=0" || exit 1
-done
+timeout -k 10 600 python -m pytest tests -x -q -m gpu > gpurun_out/pytest_gpu.log 2>&1 || { echo "pytest failed"; tail -30 gpurun_out/pytest_gpu.log; exit 1; }
+tail -1 gpurun_out/pytest_gpu.log
+QP_REPS=3 timeout -k 10 200 python tools/quick_perf.py 64 1024 || exit 1
+QP_REPS=3 timeout -k 10 200 python tools/quick_perf.py 64 2048 || exit 1
+timeout -k 10 600 python bench.py --workload C3 --no-cpu > gpurun_out/bench_c3.json 2> gpurun_out/bench_c3.err || { tail gpurun_out/bench_c3.err; exit 1; }
+cat gpurun_out/bench_c3.json
+timeout -k 10 900 python bench.py --workload C5 --no-cpu --steps 16 --warmup 2 > gpurun_out/bench_c5.json 2> gpurun_out/bench_c5.err || { tail gpurun_out/bench_c5.err; exit 1; }
+cat gpurun_out/bench_c5.json
