@@ -230,6 +230,11 @@ int mcpt_accumulate(mcpt_ctx *ctx, float *color_dev, float *hist_dev, int32_t *c
 int mcpt_set_stats(mcpt_ctx *ctx, int32_t enabled);
 int mcpt_get_stats(mcpt_ctx *ctx, mcpt_stats *out);
 
+/* HLBVH::build (MCPT/BVH/hlbvh.cpp:92-200) on the GPU: triangles and the
+ * 2n-1 output nodes are DEVICE pointers; the tree is bit-identical to
+ * mcpt_build_hlbvh's (finite vertices).  Synchronises `stream`.           */
+int mcpt_build_hlbvh_device(const mcpt_triangle *tris_dev, int64_t n, mcpt_bvh_node *nodes_dev, void *stream);
+
 /* Streaming-read bandwidth of this GPU's HBM (GB/s, best of 5 reads of
  * `bytes` after a warm-up): the measured roofline denominator SURVEY.md
  * §8(d) asks for next to the 8 TB/s spec.                                 */

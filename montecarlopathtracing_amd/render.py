@@ -192,3 +192,19 @@ def records(buf, dtype):
 
 def to_device(arr, device):
     return torch.from_numpy(np.ascontiguousarray(arr).view(np.uint8).reshape(-1)).to(device)
+
+
+def build_hlbvh_device(tris, device=0):
+    """HLBVH<CPU> built on the GPU (mcpt_build_hlbvh_device): the same 2n-1
+    BVHNode records as scene.build_hlbvh.  `tris` is a host TRIANGLE array or a
+    device byte tensor of them; returns a device byte tensor of the nodes."""
+    if isinstance(tris, np.ndarray):
+        n = len(tris)
+        tris = to_device(tris, device)
+    else:
+        n = tris.numel() // L.TRIANGLE.itemsize
+    if n == 0:
+        raise ValueError("empty scene")
+    nodes = torch.empty((2 * n - 1) * L.BVHNODE.itemsize, dtype=torch.uint8, device=tris.device)
+    L.check(L.lib().mcpt_build_hlbvh_device(L.ptr(tris), n, L.ptr(nodes), _stream()))
+    return nodes

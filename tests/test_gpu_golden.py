@@ -207,3 +207,34 @@ def test_cli_runs(tmp_path):
                        timeout=300)
     assert r.returncode == 0, r.stderr
     assert os.path.exists(tmp_path / "cbox.obj.hdr")
+
+
+def _build_cases():
+    rng = np.random.default_rng(7)
+    tri = rng.uniform(-3, 3, (50, 3, 3)).astype(np.float32)
+    dup = np.concatenate([np.repeat(tri[:1], 300, axis=0), tri])  # equal Morton codes: middle splits
+    flat = tri.copy()
+    flat[:, :, 2] = 0.0  # a flat axis: 0/0 in the code -> 0
+    cases = {"one": tri[:1], "two": tri[:2], "three": tri[:3], "dup": dup, "flat": flat,
+             "signed_zero": np.where(np.abs(tri) < 0.5, np.float32(-0.0), tri).astype(np.float32)}
+    return cases
+
+
+@pytest.mark.parametrize("name", ["cbox", "mis", "random200k", "one", "two", "three", "dup", "flat", "signed_zero"])
+def test_gpu_hlbvh_build_equals_host(name):
+    """the reference HLBVH built on the GPU is the host
+    build (hlbvh.cpp restated in mcpt_host.cpp, pinned to the C oracle) bit for bit."""
+    if name == "cbox":
+        tris = scenes.cbox().tris
+    elif name == "mis":
+        tris = scenes.mis().tris
+    elif name == "random200k":
+        tris = S.random_mesh(200_000).tris
+    else:
+        v = _build_cases()[name]
+        t = np.zeros(len(v), L.TRIANGLE)
+        t["v"][:, :, :3] = v
+        tris = S.pack_triangles(t, np.zeros(len(v), np.int32))
+    host = S.build_hlbvh(tris)
+    dev = R.records(R.build_hlbvh_device(tris), L.BVHNODE)
+    assert_bits_equal(dev, host, "hlbvh nodes")

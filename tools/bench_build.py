@@ -1,0 +1,55 @@
+"""Scene build times (build time is excluded from the render
+metric but reported): the reference HLBVH on the host (mcpt_build_hlbvh, the
+restated hlbvh.cpp) vs on the GPU (mcpt_build_hlbvh_device, same bits), and
+mcpt_scene_upload (device copies + the EXACT path's SAH search tree).
+
+    python tools/bench_build.py [C2 C5 ...]  -> one JSON line per workload
+"""
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+from bench import load_scene  # noqa: E402
+from montecarlopathtracing_amd import _lib as L  # noqa: E402
+from montecarlopathtracing_amd import render as R  # noqa: E402
+from montecarlopathtracing_amd import scene as S  # noqa: E402
+
+
+def main():
+    for wl in sys.argv[1:] or ["C2", "C5"]:
+        data, _ = load_scene(wl)
+        tris = data.tris
+        t0 = time.perf_counter()
+        host = S.build_hlbvh(tris)
+        t_host = time.perf_counter() - t0
+        dt = R.to_device(tris, 0)
+        R.build_hlbvh_device(dt)  # warm (hipCUB kernels, allocator)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        dev = R.build_hlbvh_device(dt)
+        torch.cuda.synchronize()
+        t_dev = time.perf_counter() - t0
+        same = bool(np.array_equal(R.records(dev, L.BVHNODE).view(np.uint8), host.view(np.uint8)))
+        rnd = R.Renderer(0)
+        t0 = time.perf_counter()
+        sc = rnd.upload(data)
+        torch.cuda.synchronize()
+        t_up = time.perf_counter() - t0
+        sc.close()
+        rnd.close()
+        print(json.dumps({"workload": wl, "triangles": len(tris), "hlbvh_host_s": round(t_host, 4),
+                          "hlbvh_gpu_s": round(t_dev, 4), "gpu_equals_host": same,
+                          "scene_upload_s": round(t_up, 4),
+                          "note": "scene_upload = validation + 4-wide trees (reference collapse + SAH search "
+                                  "tree, host, 16 threads) + device copies"}), flush=True)
+
+
+if __name__ == "__main__":
+    main()
