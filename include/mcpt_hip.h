@@ -235,6 +235,16 @@ int mcpt_get_stats(mcpt_ctx *ctx, mcpt_stats *out);
  * mcpt_build_hlbvh's (finite vertices).  Synchronises `stream`.           */
 int mcpt_build_hlbvh_device(const mcpt_triangle *tris_dev, int64_t n, mcpt_bvh_node *nodes_dev, void *stream);
 
+/* TreeletBVH<CPU> (MCPT/BVH/treeletBVH.cpp:343-372, the reference's
+ * "bvhtype": "treelet", scenebuild.cpp:70-73) on the GPU, in place on a
+ * DEVICE array of 2n-1 nodes as mcpt_build_hlbvh[_device] lays them out:
+ * Karras-Aila treelets of up to 7 leaves rebuilt bottom-up with the
+ * reference's heap order, subset DP and refit, bit-identical to the
+ * reference's sequential pass.  MCPT_ERR_ARG when the reference's own SAH
+ * recursion would not terminate on the tree (treeletBVH.cpp:327 quirk).
+ * Synchronises `stream`.                                                  */
+int mcpt_treelet_device(mcpt_bvh_node *nodes_dev, int64_t n_nodes, void *stream);
+
 /* Streaming-read bandwidth of this GPU's HBM (GB/s, best of 5 reads of
  * `bytes` after a warm-up): the measured roofline denominator SURVEY.md
  * §8(d) asks for next to the 8 TB/s spec.                                 */

@@ -85,6 +85,7 @@ SIGNATURES = {
     "mcpt_selfcheck_trig": (_I32, [_P, _P, _P]),
     "mcpt_measure_read_bw": (_I32, [_P, _I64, _P]),
     "mcpt_build_hlbvh_device": (_I32, [_P, _I64, _P, _P]),
+    "mcpt_treelet_device": (_I32, [_P, _I64, _P]),
 }
 
 _lib = None

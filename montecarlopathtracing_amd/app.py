@@ -49,6 +49,15 @@ class App:
         if not directory.endswith("/"):
             directory += "/"
         self.data = S.SceneData.from_obj(directory, self.cfg.GETOBJNAME(), self.material_override)
+        # SceneCL ctor (scenebuild.cpp:66-79): HLBVH, optionally restructured
+        # by the treelet pass.  "treeletGPU" runs the reference's GPU kernel
+        # (treeletBVH.cl), whose result depends on warp-synchronous races; both
+        # names run TreeletBVH<CPU>'s deterministic pass here.
+        bvhtype = self.cfg.BVHTYPE()
+        if bvhtype in ("treelet", "treeletGPU"):
+            self.data = self.data.with_nodes(R.treelet_device(self.data.nodes, self.device))
+        elif bvhtype != "hlbvh":
+            raise ValueError("BVH Not Implemented: %r" % bvhtype)  # scenebuild.cpp:78
         self.camera = S.parse_camera(cam)
         self.renderer = R.Renderer(self.device)
         self.scene = self.renderer.upload(self.data)

@@ -249,3 +249,387 @@ done:
     if (p) (void)hipFree(p);
   return rc;
 }
+
+// ===========================================================================
+// Treelet restructuring (MCPT/BVH/treeletBVH.cpp:1-387, TreeletBVH<CPU>), the
+// pass the reference applies for "bvhtype": "treelet" (scenebuild.cpp:70-73).
+//
+// The reference walks up from every leaf along the ORIGINAL parent links and
+// rebuilds a node's treelet when its second child walk arrives.  A rebuild of
+// node X only rearranges nodes inside X's original subtree, and reads only
+// that subtree, so any order that rebuilds a node after all its original
+// descendants gives the same tree.  Here: the internal nodes are grouped by
+// original depth (top-down frontier), and each depth is one launch, deepest
+// first, one wave per node.  Kernel boundaries order a child treelet's writes
+// before its ancestors' reads (no cross-XCD flags).  Inside a wave:
+//  * lane 0 grows the treelet with the reference's binary heap, written out
+//    (pop_heap = Floyd's hole descent + sift-up, push_heap = sift-up, the
+//    libstdc++ / MSVC STL algorithms; oracle/mcpt_oracle_treelet.cpp uses
+//    std::pop_heap/push_heap and the tests compare bit for bit);
+//  * the 2^n - 1 union areas are one subset per lane;
+//  * the subset DP runs one popcount class per step, one subset per lane
+//    (subsets of equal size never read each other, so the reference's
+//    sequential (popcount, value) order gives the same costs);
+//  * lane 0 rebuilds and refits (at most 6 nodes).
+// getInformation's SAH pass (treeletBVH.cpp:321-347) runs bottom-up by the
+// same depth groups; its first-leaf quirk (node n-1 is read as an internal
+// node whose children are both node `left`) is evaluated after every other
+// node off the root-to-(n-1) path, then that path, deepest first.
+// ===========================================================================
+namespace {
+
+constexpr int TL_MAX = 7;                           // treeletBVH.cpp:14
+constexpr float TL_CINN = 1.2f, TL_CTRI = 1.0f, TL_CLEAF = 0.0f;  // auxiliary.h:9-11
+
+__device__ inline float tl_area(const float *mn, const float *mx) {  // auxiliary.cpp:15-18
+  const float x = mx[0] - mn[0], y = mx[1] - mn[1], z = mx[2] - mn[2];
+  return 2.0f * (x * y + x * z + y * z);
+}
+inline float tl_area_host(const mcpt_bvh_node &b) {
+  const float x = b.bbmax[0] - b.bbmin[0], y = b.bbmax[1] - b.bbmin[1], z = b.bbmax[2] - b.bbmin[2];
+  return 2.0f * (x * y + x * z + y * z);
+}
+
+struct TlQ {
+  int id;
+  float value;
+};
+__device__ inline bool tl_less(const TlQ &a, const TlQ &b) {  // QueueNode::operator< (:36-41)
+  if (a.value < b.value) return true;
+  return a.value == b.value && a.id < b.id;
+}
+__device__ inline void tl_sift_up(TlQ *h, int hole, TlQ v) {  // __push_heap
+  int parent = (hole - 1) / 2;
+  while (hole > 0 && tl_less(h[parent], v)) {
+    h[hole] = h[parent];
+    hole = parent;
+    parent = (hole - 1) / 2;
+  }
+  h[hole] = v;
+}
+__device__ inline void tl_push(TlQ *h, int &n, TlQ v) {  // push_back + push_heap
+  h[n] = v;
+  ++n;
+  tl_sift_up(h, n - 1, v);
+}
+__device__ inline void tl_pop(TlQ *h, int &n) {  // pop_heap + pop_back
+  if (n > 1) {
+    const int len = n - 1;  // heap size after the move
+    TlQ v = h[len];
+    h[len] = h[0];
+    int hole = 0, child = 0;
+    while (child < (len - 1) / 2) {
+      child = 2 * (child + 1);
+      if (tl_less(h[child], h[child - 1])) --child;
+      h[hole] = h[child];
+      hole = child;
+    }
+    if ((len & 1) == 0 && child == (len - 2) / 2) {
+      child = 2 * (child + 1);
+      h[hole] = h[child - 1];
+      hole = child - 1;
+    }
+    tl_sift_up(h, hole, v);
+  }
+  --n;
+}
+
+// frontier expansion: the internal children of one depth's internal nodes
+__global__ void k_tl_expand(const int32_t *__restrict__ in, uint32_t count, const mcpt_bvh_node *__restrict__ nodes,
+                            int32_t *out, uint32_t *out_count) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= count) return;
+  const mcpt_bvh_node &b = nodes[in[i]];
+  int32_t c[2];
+  uint32_t k = 0;
+  for (int32_t x : {b.left, b.right})
+    if (nodes[x].left != nodes[x].right) c[k++] = x;
+  if (k) {
+    uint32_t o = atomicAdd(out_count, k);
+    for (uint32_t j = 0; j < k; ++j) out[o + j] = c[j];
+  }
+}
+
+// getInformation, leaves (the `id > size/2` test of :327: all but node n-1)
+__global__ void k_tl_sah_leaves(const mcpt_bvh_node *__restrict__ nodes, int64_t n, float root_area, float *sah) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x + n;  // [n, 2n-2]
+  if (i > 2 * n - 2) return;
+  sah[i] = (TL_CTRI + TL_CLEAF) * tl_area(nodes[i].bbmin, nodes[i].bbmax) / root_area;
+}
+
+// getInformation, one depth of internal nodes off the (n-1) path
+__global__ void k_tl_sah_level(const int32_t *__restrict__ lvl, uint32_t count, const uint8_t *__restrict__ on_path,
+                               const mcpt_bvh_node *__restrict__ nodes, float root_area, float *sah) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= count) return;
+  const int32_t x = lvl[i];
+  if (on_path[x]) return;
+  const mcpt_bvh_node &b = nodes[x];
+  sah[x] = sah[b.left] + sah[b.right] + TL_CINN * (tl_area(b.bbmin, b.bbmax)) / root_area;
+}
+
+// marks the root-to-(n-1) path; flags a cycle of the first-leaf quirk
+__global__ void k_tl_mark_path(const mcpt_bvh_node *__restrict__ nodes, int64_t n, uint8_t *on_path, int32_t *err) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  const int32_t t = nodes[n - 1].left;
+  *err = (t == n - 1) ? 1 : 0;
+  for (int32_t p = nodes[n - 1].parent; p != -1; p = nodes[p].parent) {
+    on_path[p] = 1;
+    if (p == t) *err = 1;
+  }
+}
+
+// the first leaf (read as internal, both children = node t) and its ancestors
+__global__ void k_tl_sah_path(const mcpt_bvh_node *__restrict__ nodes, int64_t n, float root_area, float *sah) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  const mcpt_bvh_node &f = nodes[n - 1];
+  sah[n - 1] = sah[f.left] + sah[f.right] + TL_CINN * (tl_area(f.bbmin, f.bbmax)) / root_area;
+  for (int32_t p = f.parent; p != -1; p = nodes[p].parent) {
+    const mcpt_bvh_node &b = nodes[p];
+    sah[p] = sah[b.left] + sah[b.right] + TL_CINN * (tl_area(b.bbmin, b.bbmax)) / root_area;
+  }
+}
+
+// reconstructTreelet (:30-318) for one depth's nodes, one 64-lane wave each
+__global__ __launch_bounds__(64) void k_tl_rebuild(const int32_t *__restrict__ lvl, uint32_t count,
+                                                    mcpt_bvh_node *nodes, float *sah, float root_area) {
+  __shared__ TlQ pq[TL_MAX + 1];
+  __shared__ int32_t freeN[TL_MAX];
+  __shared__ int npq_s, nfree_s;
+  __shared__ float area[128], cost[128];
+  __shared__ int32_t part[128];
+  __shared__ float bmn[TL_MAX][4], bmx[TL_MAX][4];
+  if (blockIdx.x >= count) return;
+  const int lane = threadIdx.x;
+  const int32_t root = lvl[blockIdx.x];
+
+  if (lane == 0) {  // grow the treelet (:44-80)
+    int n = 0, nf = 0;
+    tl_push(pq, n, TlQ{root, sah[root]});
+    while (n < TL_MAX) {
+      const TlQ mx = pq[0];
+      tl_pop(pq, n);
+      if (mx.value < 0.0f) {
+        pq[n++] = TlQ{mx.id, -1.0f};  // push_back without push_heap (:55)
+        break;
+      }
+      const int32_t l = nodes[mx.id].left, r = nodes[mx.id].right;
+      if (l == r) {
+        tl_push(pq, n, TlQ{mx.id, mx.id * (-1.0f)});
+        continue;
+      }
+      tl_push(pq, n, TlQ{l, sah[l]});
+      tl_push(pq, n, TlQ{r, sah[r]});
+      freeN[nf++] = mx.id;
+    }
+    npq_s = n;
+    nfree_s = nf;
+    for (int j = 0; j < n; ++j)
+      for (int k = 0; k < 4; ++k) bmn[j][k] = nodes[pq[j].id].bbmin[k], bmx[j][k] = nodes[pq[j].id].bbmax[k];
+  }
+  for (int s = lane; s < 128; s += 64) cost[s] = 0.0f, part[s] = 0;
+  __syncthreads();
+  const int NN = npq_s;  // pq.size() never exceeds MAX_NODE, so NOW_NODE == pq.size()
+  if (NN < 3) return;
+  const int full = (1 << NN) - 1;
+
+  // union areas (:95-119): bit k of the subset <-> pq[NN-1-k]
+  for (int s = lane + 1; s <= full; s += 64) {
+    float mn[3] = {FLT_MAX, FLT_MAX, FLT_MAX}, mx[3] = {-FLT_MAX, -FLT_MAX, -FLT_MAX};
+    for (int j = 0; j < NN; ++j) {
+      if ((s >> (NN - 1 - j)) & 1) {
+        for (int k = 0; k < 3; ++k) {
+          mx[k] = smax(mx[k], bmx[j][k]);
+          mn[k] = smin(mn[k], bmn[j][k]);
+        }
+      }
+    }
+    area[s] = tl_area(mn, mx);
+  }
+  if (lane < NN) cost[1 << lane] = sah[pq[lane].id];  // (:125-127): bit i <-> pq[i]
+  __syncthreads();
+
+  // subset DP (:158-199), one popcount class per step
+  for (int k = 2; k <= NN; ++k) {
+    for (int s = lane + 1; s <= full; s += 64) {
+      if (__builtin_popcount(s) != k) continue;
+      float cs = FLT_MAX, ps = 0.0f;
+      const int delta = (s - 1) & s;
+      int p = (-delta) & s;
+      do {
+        const float c = cost[p] + cost[s ^ p];
+        if (c < cs) {
+          cs = c;
+          ps = (float)p;
+        }
+        p = (p - delta) & s;
+      } while (p != 0);
+      cost[s] = TL_CINN * area[s] + cs;
+      part[s] = (int32_t)ps;
+    }
+    __syncthreads();
+  }
+
+  if (lane == 0) {  // rebuild (:201-291) breadth-first, then refit (:293-302)
+    struct Split {
+      int parent_code, self_code, parent_id;
+    };
+    Split a[TL_MAX], b[TL_MAX];
+    Split *cur = a, *nxt = b;
+    int ncur = 1, nnxt = 0, fnow = 1;
+    cur[0] = Split{full, part[full], freeN[0]};
+    auto leaf_of = [&](int code) { return pq[NN - 1 - (31 - __builtin_clz((unsigned)code))].id; };
+    while (ncur > 0) {
+      for (int x = 0; x < ncur; ++x) {
+        const Split i = cur[x];
+        const int lcode = part[i.self_code], rcode = part[i.self_code ^ i.parent_code];
+        const int pid = i.parent_id;
+        if (__builtin_popcount(i.self_code) == 1) {
+          const int node = leaf_of(i.self_code);
+          nodes[pid].left = node;
+          nodes[node].parent = pid;
+        } else {
+          const int f = freeN[fnow++];
+          nodes[pid].left = f;
+          nxt[nnxt++] = Split{i.self_code, lcode, f};
+          nodes[f].parent = pid;
+        }
+        const int rc = i.parent_code ^ i.self_code;
+        if (__builtin_popcount(rc) == 1) {
+          const int node = leaf_of(rc);
+          nodes[pid].right = node;
+          nodes[node].parent = pid;
+        } else {
+          const int f = freeN[fnow++];
+          nodes[pid].right = f;
+          nxt[nnxt++] = Split{rc, rcode, f};
+          nodes[f].parent = pid;
+        }
+      }
+      Split *t = cur;
+      cur = nxt;
+      nxt = t;
+      ncur = nnxt;
+      nnxt = 0;
+    }
+    for (int i = nfree_s - 1; i >= 0; --i) {
+      mcpt_bvh_node &P = nodes[freeN[i]];
+      const mcpt_bvh_node &A = nodes[P.left], &B = nodes[P.right];
+      for (int k = 0; k < 4; ++k) {
+        P.bbmax[k] = smax(A.bbmax[k], B.bbmax[k]);
+        P.bbmin[k] = smin(A.bbmin[k], B.bbmin[k]);
+      }
+      sah[freeN[i]] = sah[P.left] + sah[P.right] + TL_CINN * (tl_area(P.bbmin, P.bbmax)) / root_area;
+    }
+  }
+}
+
+}  // namespace
+
+#define TL_OK(expr)                                                                          \
+  do {                                                                                       \
+    hipError_t e_ = (expr);                                                                  \
+    if (e_ != hipSuccess) {                                                                  \
+      rc = mcpt::fail(MCPT_ERR_HIP, std::string("treelet_device: ") + #expr + ": " + hipGetErrorString(e_)); \
+      goto done;                                                                             \
+    }                                                                                        \
+  } while (0)
+
+extern "C" int mcpt_treelet_device(mcpt_bvh_node *nodes, int64_t n_nodes, void *stream) {
+  if (!nodes || n_nodes <= 0 || (n_nodes & 1) == 0)
+    return mcpt::fail(MCPT_ERR_ARG, "treelet_device: expected a 2n-1-node BVH");
+  const int64_t n = (n_nodes + 1) / 2;
+  if (n < 2) return MCPT_OK;  // a single leaf: the leaf loop finds no parent
+  if (n > (int64_t)0x3FFFFFFF) return mcpt::fail(MCPT_ERR_LIMIT, "treelet_device: too many triangles");
+  hipStream_t st = (hipStream_t)stream;
+  int rc = MCPT_OK;
+  float *sah = nullptr;
+  int32_t *lv = nullptr, *err = nullptr;
+  uint8_t *on_path = nullptr;
+  uint32_t *cnt = nullptr;
+  std::vector<uint32_t> off;
+  mcpt_bvh_node root_h;
+  int32_t err_h = 0;
+  float root_area = 0.0f;
+
+  TL_OK(hipMalloc(&sah, n_nodes * sizeof(float)));
+  TL_OK(hipMalloc(&lv, (n - 1) * sizeof(int32_t)));
+  TL_OK(hipMalloc(&on_path, n_nodes));
+  TL_OK(hipMalloc(&err, sizeof(int32_t)));
+  TL_OK(hipMalloc(&cnt, sizeof(uint32_t)));
+  TL_OK(hipMemcpyAsync(&root_h, nodes, sizeof(root_h), hipMemcpyDeviceToHost, st));
+  TL_OK(hipMemsetAsync(on_path, 0, n_nodes, st));
+  TL_OK(hipStreamSynchronize(st));
+  if (root_h.left == root_h.right) {
+    rc = mcpt::fail(MCPT_ERR_ARG, "treelet_device: node 0 must be the internal root");
+    goto done;
+  }
+  root_area = tl_area_host(root_h);  // ::rootArea, fixed before any rebuild (:351)
+  {
+    // depth groups of internal nodes, top-down
+    const int32_t zero = 0;
+    TL_OK(hipMemcpyAsync(lv, &zero, sizeof(int32_t), hipMemcpyHostToDevice, st));
+    off.push_back(0);
+    off.push_back(1);
+    for (;;) {
+      const uint32_t a = off[off.size() - 2], b = off.back();
+      if (b == a) break;
+      if (b > (uint32_t)(n - 1)) {
+        rc = mcpt::fail(MCPT_ERR_ARG, "treelet_device: node links do not form a tree");
+        goto done;
+      }
+      TL_OK(hipMemsetAsync(cnt, 0, sizeof(uint32_t), st));
+      hipLaunchKernelGGL(k_tl_expand, dim3(blocks_for(b - a, 256)), dim3(256), 0, st, lv + a, b - a, nodes, lv + b,
+                         cnt);
+      TL_OK(hipGetLastError());
+      uint32_t c = 0;
+      TL_OK(hipMemcpyAsync(&c, cnt, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+      TL_OK(hipStreamSynchronize(st));
+      if ((uint64_t)b + c > (uint64_t)(n - 1)) {
+        rc = mcpt::fail(MCPT_ERR_ARG, "treelet_device: node links do not form a tree");
+        goto done;
+      }
+      off.push_back(b + c);
+    }
+    if (off.back() != (uint32_t)(n - 1)) {
+      rc = mcpt::fail(MCPT_ERR_ARG, "treelet_device: expected n-1 internal nodes reachable from the root");
+      goto done;
+    }
+  }
+  // getInformation (:343-347)
+  hipLaunchKernelGGL(k_tl_mark_path, dim3(1), dim3(64), 0, st, nodes, n, on_path, err);
+  TL_OK(hipGetLastError());
+  TL_OK(hipMemcpyAsync(&err_h, err, sizeof(int32_t), hipMemcpyDeviceToHost, st));
+  TL_OK(hipStreamSynchronize(st));
+  if (err_h) {
+    rc = mcpt::fail(MCPT_ERR_ARG,
+                    "treelet_device: the reference's getInformation recursion does not terminate on this tree "
+                    "(leaf n-1's triangle index names one of its ancestors)");
+    goto done;
+  }
+  if (n > 1) {
+    hipLaunchKernelGGL(k_tl_sah_leaves, dim3(blocks_for(n - 1, 256)), dim3(256), 0, st, nodes, n, root_area, sah);
+    TL_OK(hipGetLastError());
+  }
+  for (size_t k = off.size() - 1; k-- > 0;) {
+    const uint32_t a = off[k], b = off[k + 1];
+    if (b == a) continue;
+    hipLaunchKernelGGL(k_tl_sah_level, dim3(blocks_for(b - a, 256)), dim3(256), 0, st, lv + a, b - a, on_path, nodes,
+                       root_area, sah);
+    TL_OK(hipGetLastError());
+  }
+  hipLaunchKernelGGL(k_tl_sah_path, dim3(1), dim3(64), 0, st, nodes, n, root_area, sah);
+  TL_OK(hipGetLastError());
+  // treelets, deepest depth first
+  for (size_t k = off.size() - 1; k-- > 0;) {
+    const uint32_t a = off[k], b = off[k + 1];
+    if (b == a) continue;
+    hipLaunchKernelGGL(k_tl_rebuild, dim3(b - a), dim3(64), 0, st, lv + a, b - a, nodes, sah, root_area);
+    TL_OK(hipGetLastError());
+  }
+  TL_OK(hipStreamSynchronize(st));
+done:
+  for (void *p : {(void *)sah, (void *)lv, (void *)on_path, (void *)err, (void *)cnt})
+    if (p) (void)hipFree(p);
+  return rc;
+}

@@ -208,3 +208,15 @@ def build_hlbvh_device(tris, device=0):
     nodes = torch.empty((2 * n - 1) * L.BVHNODE.itemsize, dtype=torch.uint8, device=tris.device)
     L.check(L.lib().mcpt_build_hlbvh_device(L.ptr(tris), n, L.ptr(nodes), _stream()))
     return nodes
+
+
+def treelet_device(nodes, device=0):
+    """TreeletBVH<CPU> (MCPT/BVH/treeletBVH.cpp:343-372, "bvhtype": "treelet")
+    run on the GPU by mcpt_treelet_device.  `nodes` is a host BVHNODE array
+    (returns a restructured host copy) or a device byte tensor (restructured
+    in place and returned)."""
+    host = isinstance(nodes, np.ndarray)
+    d = to_device(nodes, device) if host else nodes
+    n = d.numel() // L.BVHNODE.itemsize
+    L.check(L.lib().mcpt_treelet_device(L.ptr(d), n, _stream()))
+    return records(d, L.BVHNODE).copy() if host else d

@@ -96,6 +96,10 @@ class SceneData:
     def __init__(self, tris, nodes, mats):
         self.tris, self.nodes, self.mats = tris, nodes, mats
 
+    def with_nodes(self, nodes):
+        """Same triangles and materials over another BVH (e.g. a treelet pass)."""
+        return SceneData(self.tris, nodes, self.mats)
+
     @classmethod
     def from_obj(cls, directory, objname, material_override=None):
         tris, mats, idx = load_object(directory, objname)

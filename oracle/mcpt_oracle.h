@@ -47,6 +47,10 @@ void oracle_render_pixels(const mcpt_camera *cam, const mcpt_triangle *tris, con
  * (skip a node whose box starts beyond the current hit).  Default 0 =
  * the reference's exhaustive traversal. */
 void oracle_set_prune(int on);
+/* TreeletBVH<CPU> (MCPT/BVH/treeletBVH.cpp:343-372) in place on a 2n-1-node
+ * HLBVH; mcpt_oracle_treelet.cpp.  0 ok, -1 the reference's recursion would
+ * not terminate on this tree, -2 bad argument. */
+int oracle_treelet(mcpt_bvh_node *nodes, int64_t n_nodes);
 int64_t oracle_encode_hdr(int32_t w, int32_t h, const float *rgba, int32_t flip, uint8_t *out, int64_t cap);
 
 #ifdef __cplusplus

@@ -98,3 +98,10 @@ def encode_hdr(rgba, flip=True):
     buf = np.zeros(n, np.uint8)
     so().oracle_encode_hdr(i32(w), i32(h), P(a), i32(int(flip)), P(buf), i64(n))
     return buf.tobytes()
+
+
+def treelet(nodes):
+    """TreeletBVH<CPU> restated (oracle/mcpt_oracle_treelet.cpp): (status, nodes)."""
+    out = np.ascontiguousarray(nodes).copy()
+    rc = so().oracle_treelet(P(out), i64(len(out)))
+    return rc, out

@@ -1,0 +1,118 @@
+"""GPU BVH passes against their CPU restatements.
+
+TreeletBVH<CPU> (MCPT/BVH/treeletBVH.cpp, "bvhtype": "treelet") runs on the
+GPU as mcpt_treelet_device; the oracle (oracle/mcpt_oracle_treelet.cpp) is the
+reference's sequential pass written with the same std::push_heap/pop_heap
+calls.  Bar: node arrays bit-identical.  Parity note: the reference host C++
+cannot be compiled here, so the oracle is a restatement; the
+rendered images over the treelet tree are still checked bit for bit against
+the reference's own kernels (test_gpu_parity.py).
+"""
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+
+pytestmark = pytest.mark.gpu
+
+from montecarlopathtracing_amd import _lib as L  # noqa: E402
+from montecarlopathtracing_amd import render as R  # noqa: E402
+from montecarlopathtracing_amd import scene as S  # noqa: E402
+
+from . import oracle as O  # noqa: E402
+from . import scenes  # noqa: E402
+from .test_gpu_golden import _build_cases  # noqa: E402
+from .test_gpu_parity import assert_bits_equal  # noqa: E402
+
+
+def _tris(v):
+    t = np.zeros(len(v), L.TRIANGLE)
+    t["v"][:, :, :3] = v
+    return S.pack_triangles(t, np.zeros(len(v), np.int32))
+
+
+def _case(name):
+    if name == "cbox":
+        return scenes.cbox().tris
+    if name == "mis":
+        return scenes.mis().tris
+    if name == "random200k":
+        return S.random_mesh(200_000).tris
+    if name.startswith("rand"):
+        n = int(name[4:])
+        rng = np.random.default_rng(n)
+        return _tris(rng.uniform(-2, 2, (n, 3, 3)).astype(np.float32))
+    return _tris(_build_cases()[name])
+
+
+CASES = ["cbox", "mis", "random200k", "two", "three", "dup", "flat", "signed_zero"] + \
+        ["rand%d" % k for k in (4, 5, 6, 7, 8, 9, 13, 64, 1000)]
+
+
+@pytest.mark.parametrize("name", CASES)
+def test_gpu_treelet_equals_oracle(name):
+    tris = _case(name)
+    nodes = S.build_hlbvh(tris)
+    rc, ref = O.treelet(nodes)
+    if rc == -1:
+        with pytest.raises(L.MCPTError):
+            R.treelet_device(nodes)
+        return
+    assert rc == 0
+    mine = R.treelet_device(nodes)
+    assert_bits_equal(mine, ref, "treelet nodes")
+
+
+def test_gpu_treelet_on_device_built_hlbvh():
+    """The GPU pipeline end to end: HLBVH built on the GPU, then treelets, in
+    HBM, equals the oracle's pass over the host build."""
+    tris = S.random_mesh(100_000, seed=5).tris
+    d = R.build_hlbvh_device(tris)
+    R.treelet_device(d)
+    _, ref = O.treelet(S.build_hlbvh(tris))
+    assert_bits_equal(R.records(d, L.BVHNODE), ref, "device pipeline")
+
+
+def test_gpu_treelet_recursion_cycle_is_an_error():
+    n = 40
+    x = np.arange(n, dtype=np.float32)
+    v = np.zeros((n, 3, 3), np.float32)
+    v[:, 0, 0], v[:, 1, 0], v[:, 2, 0] = x, x + 0.5, x
+    v[:, 2, 1] = 0.5
+    nodes = S.build_hlbvh(_tris(v))
+    assert O.treelet(nodes)[0] == -1
+    with pytest.raises(L.MCPTError, match="does not terminate"):
+        R.treelet_device(nodes)
+
+
+@pytest.mark.parametrize("bvhtype", ["treelet", "treeletGPU"])
+def test_app_bvhtype_treelet(tmp_path, bvhtype):
+    """config "bvhtype" selects the treelet pass (scenebuild.cpp:66-79): the
+    App uploads exactly the oracle's restructured tree and renders over it."""
+    import json
+
+    from montecarlopathtracing_amd import config as C
+    from montecarlopathtracing_amd.app import App
+    obj = C.Config(scenes.CFG, configid=2).root
+    obj = json.loads(json.dumps(obj))
+    obj["config"][2]["bvhtype"] = bvhtype
+    obj["config"][2]["width"] = obj["config"][2]["height"] = 32
+    obj["config"][2]["camera"]["resolution"] = [32, 32]
+    obj["config"][2]["directory"] = scenes.ROOT + "/scenes/cbox/"
+    app = App(C.Config(obj, configid=2), out_dir=str(tmp_path), root="/")
+    app.init()
+    _, ref = O.treelet(scenes.cbox().nodes)
+    assert_bits_equal(app.data.nodes, ref, "app treelet nodes")
+    app.update(2)
+    assert app.state.count.cpu().numpy().sum() > 0
+
+
+def test_app_unknown_bvhtype_raises():
+    from montecarlopathtracing_amd import config as C
+    from montecarlopathtracing_amd.app import App
+    obj = dict(C.Config(scenes.CFG, configid=2).root)
+    obj["config"] = [dict(c) for c in obj["config"]]
+    obj["config"][2]["bvhtype"] = "sah"
+    app = App(C.Config(obj, configid=2), root=scenes.ROOT)
+    with pytest.raises(ValueError, match="BVH Not Implemented"):
+        app.init()

@@ -149,6 +149,22 @@ def test_render_frames_bitexact(rnd, name, getter, camjson, depth):
     assert_bits_equal(h_, rh, "hist")
 
 
+@needs_ref
+@pytest.mark.parametrize("name,getter,camjson,depth", [("cbox", scenes.cbox, scenes.CBOX_CAM, 6),
+                                                       ("mis", scenes.mis, scenes.MIS_CAM, 12)])
+def test_render_over_treelet_bvh_bitexact(rnd, name, getter, camjson, depth):
+    """"bvhtype": "treelet": the restructured tree changes the reference's
+    left-first visiting order (and so its tie winners); the HIP path over the
+    same tree still matches the reference kernels bit for bit."""
+    data = getter()
+    data = data.with_nodes(R.treelet_device(data.nodes))
+    _bounce_chain(rnd, data, camjson, 48, 40, 4, L.MODE_EXACT)
+    (h_, c_, s_), (rh, rc, rs) = _render_both(rnd, data, camjson, 64, 64, depth, 6, 4)
+    assert_bits_equal(c_, rc, "count")
+    assert_bits_equal(s_, rs, "seeds")
+    assert_bits_equal(h_, rh, "hist")
+
+
 NEAR_TIES = [("cbox", 0.0, scenes.CBOX_CAM), ("mis", 0.0, scenes.MIS_CAM), ("mis", 3e-6, scenes.MIS_CAM)]
 
 

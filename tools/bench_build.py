@@ -1,7 +1,9 @@
 """Scene build times (build time is excluded from the render
 metric but reported): the reference HLBVH on the host (mcpt_build_hlbvh, the
 restated hlbvh.cpp) vs on the GPU (mcpt_build_hlbvh_device, same bits), and
-mcpt_scene_upload (device copies + the EXACT path's SAH search tree).
+mcpt_scene_upload (device copies + the EXACT path's SAH search tree), and the
+treelet pass ("bvhtype": "treelet") on the GPU vs the CPU oracle's sequential
+restatement of TreeletBVH<CPU> (the reference's own algorithm, single thread).
 
     python tools/bench_build.py [C2 C5 ...]  -> one JSON line per workload
 """
@@ -37,6 +39,25 @@ def main():
         torch.cuda.synchronize()
         t_dev = time.perf_counter() - t0
         same = bool(np.array_equal(R.records(dev, L.BVHNODE).view(np.uint8), host.view(np.uint8)))
+        dn = R.build_hlbvh_device(dt)
+        R.treelet_device(dn)  # warm
+        dn = R.build_hlbvh_device(dt)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        R.treelet_device(dn)
+        torch.cuda.synchronize()
+        t_tl = time.perf_counter() - t0
+        t_tl_cpu, tl_same = None, None
+        try:
+            sys.path.insert(0, ROOT)
+            from tests import oracle as O
+            if O.available():
+                t0 = time.perf_counter()
+                rc, ref = O.treelet(host)
+                t_tl_cpu = time.perf_counter() - t0
+                tl_same = bool(rc == 0 and np.array_equal(R.records(dn, L.BVHNODE).view(np.uint8), ref.view(np.uint8)))
+        except ImportError:
+            pass
         rnd = R.Renderer(0)
         t0 = time.perf_counter()
         sc = rnd.upload(data)
@@ -46,7 +67,9 @@ def main():
         rnd.close()
         print(json.dumps({"workload": wl, "triangles": len(tris), "hlbvh_host_s": round(t_host, 4),
                           "hlbvh_gpu_s": round(t_dev, 4), "gpu_equals_host": same,
-                          "scene_upload_s": round(t_up, 4),
+                          "scene_upload_s": round(t_up, 4), "treelet_gpu_s": round(t_tl, 4),
+                          "treelet_cpu_oracle_s": None if t_tl_cpu is None else round(t_tl_cpu, 4),
+                          "treelet_gpu_equals_oracle": tl_same,
                           "note": "scene_upload = validation + 4-wide trees (reference collapse + SAH search "
                                   "tree, host, 16 threads) + device copies"}), flush=True)
 
