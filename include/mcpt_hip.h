@@ -177,6 +177,11 @@ int mcpt_build_hlbvh(const mcpt_triangle *tris, int64_t n, mcpt_bvh_node *nodes)
 /* Max DFS stack depth the reference traversal needs on this tree.      */
 int mcpt_bvh_stack_depth(const mcpt_bvh_node *nodes, int64_t n_nodes, int32_t *depth);
 
+/* BVH::TEST::SAH (bvhtest.cpp:97-108), the "testbvh" SAH line: the float
+ * result (Cinn * area of nodes [0, size/2) + Ctri * area of the rest, summed
+ * in double, over the root's area) widened to double.                     */
+int mcpt_bvh_sah(const mcpt_bvh_node *nodes, int64_t n_nodes, double *sah);
+
 /* ThirdPartyWrapper::outputPicture (thirdpartywrapper.cpp:14-23):
  * stbi_write_hdr with vertical flip, 4 components in, RGB out.           */
 int mcpt_write_hdr(const char *path, int32_t width, int32_t height,
@@ -244,6 +249,21 @@ int mcpt_build_hlbvh_device(const mcpt_triangle *tris_dev, int64_t n, mcpt_bvh_n
  * recursion would not terminate on the tree (treeletBVH.cpp:327 quirk).
  * Synchronises `stream`.                                                  */
 int mcpt_treelet_device(mcpt_bvh_node *nodes_dev, int64_t n_nodes, void *stream);
+
+/* BVH quality metrics of "testbvh" (bvhtest.cpp:448-530), on the GPU.
+ * EPO_GPU (bvhtest.cpp:288-321 + kernels/EPO.cl:133-197): per-triangle EPO
+ * area and triangle area into the caller's DEVICE arrays (n_tris floats
+ * each), bit-identical to the reference kernel; *epo (optional) = their
+ * double sums in index order, divided, as the float EPO_GPU returns.
+ * *clip_overflows (optional) counts triangles whose clipped polygon exceeds
+ * the reference kernel's 8-entry arrays (undefined behaviour there).       */
+int mcpt_bvh_epo_device(const mcpt_bvh_node *nodes_dev, const mcpt_triangle *tris_dev, int64_t n_tris,
+                        float *epo_dev, float *area_dev, double *epo, uint64_t *clip_overflows, void *stream);
+/* LCV (bvhtest.cpp:324-444): leaves hit per pixel-centre camera ray into
+ * counts_dev (width*height u32, index i*height + j as the reference pushes
+ * its rays), *lcv (optional) = their standard deviation (float result).    */
+int mcpt_bvh_lcv_device(const mcpt_bvh_node *nodes_dev, int64_t n_nodes, const mcpt_camera *cam,
+                        int32_t width, int32_t height, uint32_t *counts_dev, double *lcv, void *stream);
 
 /* Streaming-read bandwidth of this GPU's HBM (GB/s, best of 5 reads of
  * `bytes` after a warm-up): the measured roofline denominator SURVEY.md

@@ -1,4 +1,5 @@
-"""Command line: render a reference config.json on the GPU(s) and write the .hdr.
+"""Command line: render a reference config.json on the GPU(s) and write the .hdr,
+or, for a "testbvh" / "testall" entry, print the BVH metrics (main.cpp:11-25).
 
     python -m montecarlopathtracing_amd [config.json] [--configid N] [--out DIR]
     torchrun --nproc-per-node 8 -m montecarlopathtracing_amd config.json   (row-stripe tiles)
@@ -16,6 +17,12 @@ def main(argv=None):
     ap.add_argument("--out", default=".")
     ap.add_argument("--frames", type=int, default=None, help="override attempt+1 frames")
     a = ap.parse_args(argv)
+    from . import config as C
+    cfg = C.Config(a.config, a.configid)
+    if cfg.TESTALL() or cfg.TESTBVH():
+        from . import bvhtest
+        bvhtest.run(cfg, root=os.path.dirname(os.path.abspath(a.config)))
+        return 0
     ws = int(os.environ.get("WORLD_SIZE", "1"))
     if ws > 1:
         return _main_dist(a)
@@ -46,6 +53,10 @@ def _main_dist(a):
     root = os.path.dirname(os.path.abspath(a.config))
     over = S.diffuse_only if cfg.entry.get("materials") == "diffuse_only" else None
     data = S.SceneData.from_obj(os.path.join(root, cfg.GETDIRECTORY()), cfg.GETOBJNAME(), over)
+    if cfg.BVHTYPE() in ("treelet", "treeletGPU"):
+        data = data.with_nodes(R.treelet_device(data.nodes, local))
+    elif cfg.BVHTYPE() != "hlbvh":
+        raise ValueError("BVH Not Implemented: %r" % cfg.BVHTYPE())
     rnd = R.Renderer(local)
     sc = rnd.upload(data)
     w, h = cfg.WIDTH(), cfg.HEIGHT()

@@ -86,6 +86,9 @@ SIGNATURES = {
     "mcpt_measure_read_bw": (_I32, [_P, _I64, _P]),
     "mcpt_build_hlbvh_device": (_I32, [_P, _I64, _P, _P]),
     "mcpt_treelet_device": (_I32, [_P, _I64, _P]),
+    "mcpt_bvh_sah": (_I32, [_P, _I64, _P]),
+    "mcpt_bvh_epo_device": (_I32, [_P, _P, _I64, _P, _P, _P, _P, _P]),
+    "mcpt_bvh_lcv_device": (_I32, [_P, _I64, _P, _I32, _I32, _P, _P, _P]),
 }
 
 _lib = None
@@ -98,6 +101,14 @@ def lib():
         if not os.path.exists(LIB_PATH):
             raise MCPTError("libmcpt_hip.so not built: run __graft_entry__.build() "
                             "or make -C montecarlopathtracing_amd/csrc (%s missing)" % LIB_PATH)
+        # torch ships its own HIP runtime; the library must bind to that same
+        # instance (device tensors cross the ABI), so torch is loaded first.
+        # Loading the library first makes torch reuse /opt/rocm's runtime by
+        # soname and leaves one of the two without a device.
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
         so = ctypes.CDLL(LIB_PATH)
         for name, (res, args) in SIGNATURES.items():
             fn = getattr(so, name)

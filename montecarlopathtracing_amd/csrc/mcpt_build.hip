@@ -21,6 +21,7 @@
 
 #include <algorithm>
 #include <cfloat>
+#include <cmath>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -631,5 +632,115 @@ extern "C" int mcpt_treelet_device(mcpt_bvh_node *nodes, int64_t n_nodes, void *
 done:
   for (void *p : {(void *)sah, (void *)lv, (void *)on_path, (void *)err, (void *)cnt})
     if (p) (void)hipFree(p);
+  return rc;
+}
+
+// ===========================================================================
+// LCV, the leaf-count-variance metric of "testbvh" (MCPT/bvhtest.cpp:324-444):
+// one un-normalised pixel-centre ray per pixel, (i + 0.5f)/W - 0.5f across
+// and (j + 0.5f)/H - 0.5f up, from the camera centre; count the leaves whose
+// box (and every ancestor's) the ray's slab test accepts with tmin 0.001f,
+// no closest-hit pruning; LCV = standard deviation of the counts.  The count
+// is a set size, so the visiting order does not matter.  Host float
+// semantics (this file: -ffp-contract=off, IEEE division, std::min/std::max).
+// ===========================================================================
+namespace {
+
+constexpr int LCV_STACK = 256;
+
+__global__ void k_lcv(const mcpt_bvh_node *__restrict__ nodes, float cx, float cy, float cz, float dx, float dy,
+                      float dz, float hx, float hy, float hz, float ux, float uy, float uz, int32_t width,
+                      int32_t height, uint32_t *counts, int32_t *overflow) {
+  const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;  // i * height + j (push order)
+  if (k >= (int64_t)width * height) return;
+  const int32_t i = (int32_t)(k / height), j = (int32_t)(k % height);
+  const float temp1 = (i + 0.5f) / width - 0.5f;
+  const float temp2 = (j + 0.5f) / height - 0.5f;
+  // distance * direction + temp1 * horizontal + temp2 * up (cl_float4 operators)
+  const float o[3] = {cx, cy, cz};
+  const float d[3] = {dx + temp1 * hx + temp2 * ux, dy + temp1 * hy + temp2 * uy, dz + temp1 * hz + temp2 * uz};
+  int32_t stack[LCV_STACK];
+  int sp = 0;
+  int32_t cur = 0;
+  uint32_t ans = 0;
+  for (;;) {
+    const mcpt_bvh_node &b = nodes[cur];
+    float tmn[3], tmx[3];
+    for (int a = 0; a < 3; ++a) {
+      const float off1 = (b.bbmin[a] - o[a]) / d[a];
+      const float off2 = (b.bbmax[a] - o[a]) / d[a];
+      tmn[a] = smin(off1, off2);
+      tmx[a] = smax(off1, off2);
+    }
+    const float tnear = smax(smax(tmn[0], tmn[1]), tmn[2]);
+    const float tfar = smin(smin(tmx[0], tmx[1]), tmx[2]);
+    const bool hit = !(tfar < tnear || tfar < 0.001f);
+    if (hit && b.left == b.right) {
+      ++ans;
+    } else if (hit) {
+      if (sp == LCV_STACK) {
+        *overflow = 1;
+        break;
+      }
+      stack[sp++] = b.right;
+      cur = b.left;
+      continue;
+    }
+    if (sp == 0) break;
+    cur = stack[--sp];
+  }
+  counts[k] = ans;
+}
+
+}  // namespace
+
+#define LCV_OK(expr)                                                                         \
+  do {                                                                                       \
+    hipError_t e_ = (expr);                                                                  \
+    if (e_ != hipSuccess) {                                                                  \
+      rc = mcpt::fail(MCPT_ERR_HIP, std::string("bvh_lcv_device: ") + #expr + ": " + hipGetErrorString(e_)); \
+      goto done;                                                                             \
+    }                                                                                        \
+  } while (0)
+
+extern "C" int mcpt_bvh_lcv_device(const mcpt_bvh_node *nodes_dev, int64_t n_nodes, const mcpt_camera *cam,
+                                   int32_t width, int32_t height, uint32_t *counts_dev, double *lcv_out,
+                                   void *stream) {
+  if (!nodes_dev || n_nodes <= 0 || !cam || width <= 0 || height <= 0 || !counts_dev)
+    return mcpt::fail(MCPT_ERR_ARG, "bvh_lcv_device: bad argument");
+  hipStream_t st = (hipStream_t)stream;
+  int rc = MCPT_OK;
+  int32_t *ovf = nullptr, ovf_h = 0;
+  const int64_t n = (int64_t)width * height;
+  std::vector<uint32_t> c;
+  const float distance = 0.5f / std::tan(cam->arg / 2);  // bvhtest.cpp:415 (the float overload)
+  float dd[3];
+  for (int a = 0; a < 3; ++a) dd[a] = distance * cam->direction[a];
+  LCV_OK(hipMalloc(&ovf, sizeof(int32_t)));
+  LCV_OK(hipMemsetAsync(ovf, 0, sizeof(int32_t), st));
+  hipLaunchKernelGGL(k_lcv, dim3(blocks_for(n, 256)), dim3(256), 0, st, nodes_dev, cam->center[0], cam->center[1],
+                     cam->center[2], dd[0], dd[1], dd[2], cam->horizontal[0], cam->horizontal[1], cam->horizontal[2],
+                     cam->up[0], cam->up[1], cam->up[2], width, height, counts_dev, ovf);
+  LCV_OK(hipGetLastError());
+  LCV_OK(hipMemcpyAsync(&ovf_h, ovf, sizeof(int32_t), hipMemcpyDeviceToHost, st));
+  LCV_OK(hipStreamSynchronize(st));
+  if (ovf_h) {
+    rc = mcpt::fail(MCPT_ERR_LIMIT, "bvh_lcv_device: tree deeper than the 256-entry traversal stack");
+    goto done;
+  }
+  if (lcv_out) {  // bvhtest.cpp:430-443
+    c.resize(n);
+    LCV_OK(hipMemcpy(c.data(), counts_dev, n * sizeof(uint32_t), hipMemcpyDeviceToHost));
+    double En = 0.0, En2 = 0.0;
+    for (uint32_t x : c) {
+      En += (double)x;
+      En2 += (double)((uint64_t)x * x);
+    }
+    En /= (double)n;
+    En2 /= (double)n;
+    *lcv_out = (double)(float)std::sqrt(En2 - En * En);  // LCV returns float
+  }
+done:
+  if (ovf) (void)hipFree(ovf);
   return rc;
 }

@@ -563,6 +563,24 @@ extern "C" int mcpt_bvh_stack_depth(const mcpt_bvh_node *nodes, int64_t n_nodes,
   return MCPT_OK;
 }
 
+// BVH::TEST::SAH (bvhtest.cpp:97-108): float products summed in double,
+// Cinn for nodes [0, size/2), Ctri for the rest, over the root's area.
+extern "C" int mcpt_bvh_sah(const mcpt_bvh_node *nodes, int64_t n_nodes, double *out) {
+  if (!nodes || n_nodes <= 0 || !out) return fail(MCPT_ERR_ARG, "bvh_sah: bad argument");
+  auto area = [](const mcpt_bvh_node &b) {  // auxiliary.cpp:15-18
+    const float x = b.bbmax[0] - b.bbmin[0], y = b.bbmax[1] - b.bbmin[1], z = b.bbmax[2] - b.bbmin[2];
+    return 2.0f * (x * y + x * z + y * z);
+  };
+  const float cinn = 1.2f, ctri = 1.0f;  // auxiliary.h:9-11
+  double sah = 0.0f;
+  const size_t size = (size_t)n_nodes;
+  for (size_t i = 0; i < (size >> 1); ++i) sah += cinn * area(nodes[i]);
+  for (size_t i = (size >> 1); i < size; ++i) sah += ctri * area(nodes[i]);
+  sah /= area(nodes[0]);
+  *out = (double)(float)sah;  // SAH returns float
+  return MCPT_OK;
+}
+
 // ---------------------------------------------------------------------- HDR
 namespace {
 

@@ -71,20 +71,28 @@ __device__ inline f4 cl_normalize(f4 p) {
   }
   return q * __ocml_rsqrt_f32(l2);
 }
-// length(float4): opencl.bc _Z6lengthDv4_f (sqrt with !fpmath 3.0 = OpenCL default)
+// OpenCL's default sqrt: llvm.sqrt with !fpmath 3.0, which gfx950 lowers to
+// v_sqrt_f32 with denormal range scaling (x < 2^-126: sqrt(x * 2^32) * 2^-16).
+// Written out with the raw instruction because LLVM drops !fpmath when it
+// hoists or speculates a sqrt, and then emits the correctly rounded sequence.
+__device__ inline float cl_sqrt(float x) {
+  const bool s = x < 0x1p-126f;
+  const float r = __builtin_amdgcn_sqrtf(__builtin_amdgcn_ldexpf(x, s ? 32 : 0));
+  return __builtin_amdgcn_ldexpf(r, s ? -16 : 0);
+}
+// length(float4): opencl.bc _Z6lengthDv4_f
 __device__ inline float cl_length4(f4 p) {
   float l2 = cl_dot4(p, p);
   if (l2 < 0x1p-126f) {
     f4 q = p * 0x1p86f;
-    return __builtin_sqrtf(cl_dot4(q, q)) * 0x1p-86f;
+    return cl_sqrt(cl_dot4(q, q)) * 0x1p-86f;
   }
   if (l2 == __builtin_inff()) {
     f4 q = p * 0x1p-66f;
-    return __builtin_sqrtf(cl_dot4(q, q)) * 0x1p66f;
+    return cl_sqrt(cl_dot4(q, q)) * 0x1p66f;
   }
-  return __builtin_sqrtf(l2);
+  return cl_sqrt(l2);
 }
-__device__ inline float cl_sqrt(float x) { return __builtin_sqrtf(x); }  // llvm.sqrt !fpmath 3.0
 __device__ inline float cl_pow(float x, float y) { return __ocml_pow_f32(x, y); }
 __device__ inline float cl_cos(float x) { return __ocml_cos_f32(x); }
 __device__ inline float cl_sin(float x) { return __ocml_sin_f32(x); }

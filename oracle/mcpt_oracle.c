@@ -761,3 +761,183 @@ int64_t oracle_encode_hdr(int32_t w, int32_t h, const float *rgba, int32_t flip,
   free(scr);
   return s.n;
 }
+
+/* ----------------------------------------------- BVH metrics (testbvh) */
+static float host_area(const mcpt_bvh_node *b) { /* auxiliary.cpp:15-18 */
+  float x = b->bbmax[0] - b->bbmin[0], y = b->bbmax[1] - b->bbmin[1], z = b->bbmax[2] - b->bbmin[2];
+  return 2.0f * (x * y + x * z + y * z);
+}
+
+float oracle_bvh_sah(const mcpt_bvh_node *node, int64_t size) { /* bvhtest.cpp:97-108 */
+  double sahAns = 0.0f;
+  for (int64_t i = 0; i < (size >> 1); ++i) sahAns += 1.2f * host_area(&node[i]);
+  for (int64_t i = (size >> 1); i < size; ++i) sahAns += 1.0f * host_area(&node[i]);
+  sahAns /= host_area(&node[0]);
+  return (float)sahAns;
+}
+
+/* LCV (bvhtest.cpp:324-444), literally: rays pushed i (width) outer, j inner;
+ * cl_float4 host operators; intersectBox with std::min/std::max. */
+static int lcv_box(const float *o, const float *d, const mcpt_bvh_node *b) { /* bvhtest.cpp:23-34 */
+  float mn[3], mx[3];
+  for (int a = 0; a < 3; ++a) {
+    float off1 = (b->bbmin[a] - o[a]) / d[a];
+    float off2 = (b->bbmax[a] - o[a]) / d[a];
+    mn[a] = (off2 < off1) ? off2 : off1;
+    mx[a] = (off1 < off2) ? off2 : off1;
+  }
+  float t0 = (mn[1] < mn[0]) ? mn[0] : mn[1]; /* std::max(a, b) = (a < b) ? b : a */
+  t0 = (t0 < mn[2]) ? mn[2] : t0;
+  float t1 = (mx[1] < mx[0]) ? mx[1] : mx[0]; /* std::min(a, b) = (b < a) ? b : a */
+  t1 = (mx[2] < t1) ? mx[2] : t1;
+  return !(t1 < t0 || t1 < 0.001f);
+}
+
+float oracle_bvh_lcv(const mcpt_bvh_node *node, int64_t n_nodes, const mcpt_camera *cam, int32_t W, int32_t H,
+                     uint32_t *counts) {
+  int32_t *stack = malloc(sizeof(int32_t) * (size_t)(n_nodes + 1));
+  double En = 0.0, En2 = 0.0;
+  const float distance = 0.5f / tanf(cam->arg / 2);
+  for (int32_t i = 0; i < W; ++i) {
+    for (int32_t j = 0; j < H; ++j) {
+      float temp1 = (i + 0.5f) / W - 0.5f;
+      float temp2 = (j + 0.5f) / H - 0.5f;
+      float o[3], d[3];
+      for (int a = 0; a < 3; ++a) {
+        o[a] = cam->center[a];
+        d[a] = distance * cam->direction[a] + temp1 * cam->horizontal[a] + temp2 * cam->up[a];
+      }
+      uint64_t ans = 0;
+      int64_t sp = 0;
+      int32_t pt = 0;
+      for (;;) {
+        if (lcv_box(o, d, &node[pt])) {
+          if (node[pt].left == node[pt].right) {
+            ++ans;
+          } else {
+            stack[sp++] = node[pt].right;
+            pt = node[pt].left;
+            continue;
+          }
+        }
+        if (sp == 0) break;
+        pt = stack[--sp];
+      }
+      if (counts) counts[(int64_t)i * H + j] = (uint32_t)ans;
+      En += (double)ans;
+      En2 += (double)(ans * ans);
+    }
+  }
+  free(stack);
+  En /= (double)W * H;
+  En2 /= (double)W * H;
+  return (float)sqrt(En2 - En * En);
+}
+
+/* EPO.cl:1-197 calculateEPO on the CPU: fmaf where OpenCL contracts, libm
+ * sqrtf and IEEE '/' for the GPU's 3-ulp sqrt / 2.5-ulp division (so values
+ * agree to a few ulp, not bit for bit: tests state the tolerance). */
+typedef struct {
+  float s[3];
+} v3_t;
+static float o_len3(const float *a) {
+  float l2 = fmaf(a[2], a[2], fmaf(a[1], a[1], a[0] * a[0]));
+  if (l2 < FLT_MIN) {
+    float q[3] = {a[0] * 0x1p86f, a[1] * 0x1p86f, a[2] * 0x1p86f};
+    return sqrtf(fmaf(q[2], q[2], fmaf(q[1], q[1], q[0] * q[0]))) * 0x1p-86f;
+  }
+  if (isinf(l2)) {
+    float q[3] = {a[0] * 0x1p-66f, a[1] * 0x1p-66f, a[2] * 0x1p-66f};
+    return sqrtf(fmaf(q[2], q[2], fmaf(q[1], q[1], q[0] * q[0]))) * 0x1p66f;
+  }
+  return sqrtf(l2);
+}
+static float o_cross_len(const float *a, const float *b) {
+  float c[3] = {fmaf(a[1], b[2], b[1] * -a[2]), fmaf(a[2], b[0], b[2] * -a[0]), fmaf(a[0], b[1], b[0] * -a[1])};
+  return o_len3(c);
+}
+static void o_round_tr(v3_t *pts, int *size, int axis, float pos, int arg) {
+  if (*size == 0) return;
+  v3_t buf[32];
+  int bs = *size, ins[32], n = 0;
+  for (int i = 0; i < bs; ++i) buf[i] = pts[i];
+  for (int i = 0; i < bs; ++i) ins[i] = arg > 0 ? (buf[i].s[axis] >= pos) : (buf[i].s[axis] <= pos);
+  for (int i = 0; i < bs; ++i) {
+    int i1 = (i + 1 == bs) ? 0 : i + 1;
+    if (!ins[i] && !ins[i1]) continue;
+    if (ins[i] && ins[i1]) {
+      if (n < 32) pts[n] = buf[i];
+      ++n;
+      continue;
+    }
+    if (ins[i]) {
+      if (n < 32) pts[n] = buf[i];
+      ++n;
+    }
+    float dir[3] = {buf[i1].s[0] - buf[i].s[0], buf[i1].s[1] - buf[i].s[1], buf[i1].s[2] - buf[i].s[2]};
+    float t = (pos - buf[i].s[axis]) / dir[axis];
+    v3_t p = {{fmaf(t, dir[0], buf[i].s[0]), fmaf(t, dir[1], buf[i].s[1]), fmaf(t, dir[2], buf[i].s[2])}};
+    if (n < 32) pts[n] = p;
+    ++n;
+  }
+  *size = n < 32 ? n : 32;
+}
+static float o_intersect(const mcpt_triangle *tr, const float *mn, const float *mx) {
+  int in[3];
+  for (int k = 0; k < 3; ++k) {
+    const float *p = tr->v[k];
+    in[k] = p[0] >= mn[0] && p[0] <= mx[0] && p[1] >= mn[1] && p[1] <= mx[1] && p[2] >= mn[2] && p[2] <= mx[2];
+  }
+  if (in[0] && in[1] && in[2]) {
+    float e1[3], e2[3];
+    for (int a = 0; a < 3; ++a) e1[a] = tr->v[1][a] - tr->v[0][a], e2[a] = tr->v[2][a] - tr->v[0][a];
+    return o_cross_len(e1, e2) * 0.5f;
+  }
+  v3_t pts[32];
+  int n = 3;
+  for (int k = 0; k < 3; ++k)
+    for (int a = 0; a < 3; ++a) pts[k].s[a] = tr->v[k][a];
+  for (int a = 0; a < 3; ++a) o_round_tr(pts, &n, a, mn[a], 1);
+  for (int a = 0; a < 3; ++a) o_round_tr(pts, &n, a, mx[a], -1);
+  float ans = 0.0f;
+  if (n < 2) return ans;
+  for (int i = 1; i < n - 1; ++i) {
+    float x1[3], x2[3];
+    for (int a = 0; a < 3; ++a) x1[a] = pts[i].s[a] - pts[0].s[a], x2[a] = pts[i + 1].s[a] - pts[0].s[a];
+    ans = fmaf(o_cross_len(x1, x2), 0.5f, ans);
+  }
+  return ans;
+}
+
+void oracle_bvh_epo(const mcpt_bvh_node *bvh, const mcpt_triangle *tris, int64_t num, float *epo, float *area) {
+#pragma omp parallel for schedule(dynamic, 64)
+  for (int64_t gid = 0; gid < num; ++gid) {
+    int64_t my = gid + num - 1;
+    const mcpt_triangle *tr = &tris[bvh[my].left];
+    float e = 0.0f;
+    int anc[256], an = 1, stk[256], sp = 1;
+    anc[0] = (int)my;
+    for (int p = bvh[my].parent; p != -1 && an < 256; p = bvh[p].parent) anc[an++] = p;
+    stk[0] = 0;
+    while (sp > 0) {
+      int now = stk[--sp], skip = 0;
+      const mcpt_bvh_node *b = &bvh[now];
+      for (int i = 0; i < an; ++i)
+        if (now == anc[i]) {
+          if (b->left != b->right && sp + 2 <= 256) stk[sp++] = b->right, stk[sp++] = b->left;
+          skip = 1;
+          break;
+        }
+      if (skip) continue;
+      float ta = o_intersect(tr, b->bbmin, b->bbmax);
+      if (ta > 0) {
+        e = fmaf(ta, (now >= num - 1) ? 1.0f : 1.2f, e);
+        if (b->left != b->right && sp + 2 <= 256) stk[sp++] = b->right, stk[sp++] = b->left;
+      }
+    }
+    epo[gid] = e;
+    float e1[3], e2[3];
+    for (int a = 0; a < 3; ++a) e1[a] = tr->v[1][a] - tr->v[0][a], e2[a] = tr->v[2][a] - tr->v[0][a];
+    area[gid] = o_cross_len(e1, e2) * 0.5f;
+  }
+}

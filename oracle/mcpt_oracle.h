@@ -51,6 +51,12 @@ void oracle_set_prune(int on);
  * HLBVH; mcpt_oracle_treelet.cpp.  0 ok, -1 the reference's recursion would
  * not terminate on this tree, -2 bad argument. */
 int oracle_treelet(mcpt_bvh_node *nodes, int64_t n_nodes);
+/* testbvh metrics (bvhtest.cpp): SAH :97-108, LCV :324-444 (counts optional,
+ * index i*H + j), EPO_GPU's kernel EPO.cl:133-197 per triangle. */
+float oracle_bvh_sah(const mcpt_bvh_node *nodes, int64_t n_nodes);
+float oracle_bvh_lcv(const mcpt_bvh_node *nodes, int64_t n_nodes, const mcpt_camera *cam, int32_t w, int32_t h,
+                     uint32_t *counts);
+void oracle_bvh_epo(const mcpt_bvh_node *nodes, const mcpt_triangle *tris, int64_t n_tris, float *epo, float *area);
 int64_t oracle_encode_hdr(int32_t w, int32_t h, const float *rgba, int32_t flip, uint8_t *out, int64_t cap);
 
 #ifdef __cplusplus

@@ -1,7 +1,7 @@
 // ref_runner.hip — TEST INFRASTRUCTURE ONLY (never linked into the product).
 //
 // Runs the reference's own OpenCL kernels — MonteCarloPathTracing/kernels/
-// {rayGenerator,intersect,shade,history}.cl with objdef.h prepended, compiled
+// {rayGenerator,intersect,shade,history,EPO}.cl with objdef.h prepended, compiled
 // UNMODIFIED for gfx950 by ROCm's OpenCL C compiler (oracle/Makefile, default
 // OpenCL build options exactly as OpenCLBasic::createProgramFromFileWithHeader
 // passes them, MCPT/oclbasic.cpp:167-183) — on the GPU through the HIP module
@@ -267,6 +267,30 @@ int ref_render(const mcpt_camera *cam, const mcpt_triangle *tris, int64_t nt, co
   TRY(ds.down(seeds));
   TRY(dhist.down(hist_out));
   TRY(dn.down(count_out));
+  return 0;
+}
+
+// EPO.cl calculateEPO over an NDRange of n_tris (bvhtest.cpp:288-321 EPO_GPU):
+// per-leaf EPO area and triangle area, as the reference's host reads them back
+int ref_epo(const mcpt_bvh_node *nodes, int64_t nn, const mcpt_triangle *tris, int64_t nt, float *epo_out,
+            float *area_out) {
+  hipFunction_t f;
+  TRY(get_fn("EPO.co", "calculateEPO", &f));
+  Dev<mcpt_bvh_node> db;
+  Dev<mcpt_triangle> dt;
+  Dev<float> de, da;
+  TRY(db.alloc(nn));
+  TRY(db.up(nodes));
+  TRY(dt.alloc(nt));
+  TRY(dt.up(tris));
+  TRY(de.alloc(nt));
+  TRY(da.alloc(nt));
+  uint32_t num = (uint32_t)nt;
+  void *args[] = {&db.p, &dt.p, &de.p, &da.p, &num};
+  TRY(launch1d(f, nt, args));
+  CK(hipDeviceSynchronize());
+  TRY(de.down(epo_out));
+  TRY(da.down(area_out));
   return 0;
 }
 

@@ -23,6 +23,8 @@ def so():
     if _so is None:
         _so = ctypes.CDLL(PATH)
         _so.oracle_encode_hdr.restype = ctypes.c_int64
+        _so.oracle_bvh_sah.restype = ctypes.c_float
+        _so.oracle_bvh_lcv.restype = ctypes.c_float
     return _so
 
 
@@ -105,3 +107,22 @@ def treelet(nodes):
     out = np.ascontiguousarray(nodes).copy()
     rc = so().oracle_treelet(P(out), i64(len(out)))
     return rc, out
+
+
+def bvh_sah(nodes):
+    return so().oracle_bvh_sah(P(np.ascontiguousarray(nodes)), i64(len(nodes)))
+
+
+def bvh_lcv(nodes, cam, w, h):
+    """(LCV, per-ray leaf counts indexed i*h + j)."""
+    counts = np.zeros(w * h, np.uint32)
+    v = so().oracle_bvh_lcv(P(np.ascontiguousarray(nodes)), i64(len(nodes)), P(cam), i32(w), i32(h), P(counts))
+    return v, counts
+
+
+def bvh_epo(nodes, tris):
+    """Per-triangle (EPO area, triangle area) of EPO.cl, CPU restatement."""
+    n = len(tris)
+    e, a = np.zeros(n, np.float32), np.zeros(n, np.float32)
+    so().oracle_bvh_epo(P(np.ascontiguousarray(nodes)), P(np.ascontiguousarray(tris)), i64(n), P(e), P(a))
+    return e, a

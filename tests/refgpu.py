@@ -25,7 +25,7 @@ def so():
     if _so is None:
         s = ctypes.CDLL(os.path.join(REF_DIR, "libref_runner.so"))
         s.ref_last_error.restype = ctypes.c_char_p
-        for n in ("ref_init", "ref_generate", "ref_intersect", "ref_shade", "ref_accumulate", "ref_render"):
+        for n in ("ref_init", "ref_generate", "ref_intersect", "ref_shade", "ref_accumulate", "ref_render", "ref_epo"):
             getattr(s, n).restype = ctypes.c_int
         if s.ref_init(REF_DIR.encode()) != 0:
             raise RuntimeError(s.ref_last_error().decode())
@@ -79,3 +79,13 @@ def render(data, cam, w, h, max_depth, frames, max_attempt, seeds):
                         P(data.mats), i32(len(data.mats)), i32(w), i32(h), i32(max_depth), i32(frames),
                         i32(max_attempt), P(seeds), P(hist), P(count)))
     return hist, count, seeds
+
+
+def epo(nodes, tris):
+    """EPO.cl calculateEPO (the reference's EPO_GPU kernel): per-triangle
+    (EPO area, triangle area)."""
+    n = len(tris)
+    e, a = np.zeros(n, np.float32), np.zeros(n, np.float32)
+    _ck(so().ref_epo(P(np.ascontiguousarray(nodes)), i64(len(nodes)), P(np.ascontiguousarray(tris)), i64(n), P(e),
+                     P(a)))
+    return e, a

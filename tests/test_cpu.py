@@ -377,3 +377,77 @@ def test_oracle_treelet_reports_the_reference_recursion_cycle():
     assert nodes[n - 1]["left"] == 0  # leaf n-1 holds triangle 0 = the root's index
     rc, _ = O.treelet(nodes)
     assert rc == -1
+
+
+# ------------------------------------------------------ testbvh metrics
+@pytest.mark.parametrize("name", ["cbox", "mis"])
+def test_sah_metric_product_equals_oracle(name):
+    """BVH::TEST::SAH (bvhtest.cpp:97-108): product (host C++) = oracle (C)."""
+    from montecarlopathtracing_amd import bvhtest as B
+    nodes = getattr(scenes, name)().nodes
+    for nd in (nodes, O.treelet(nodes)[1]):
+        assert np.float32(B.sah(nd)) == np.float32(O.bvh_sah(nd))
+        assert abs(B.sah(nd) - _sah_metric(nd)) < 1e-5 * _sah_metric(nd)
+
+
+def test_oracle_lcv_counts_are_leaf_box_hits():
+    """LCV's per-ray count (bvhtest.cpp:332-357) = leaves whose box and every
+    ancestor's box pass the slab test; checked by brute force on a small tree."""
+    rng = np.random.default_rng(9)
+    v = rng.uniform(0, 10, (60, 3, 3)).astype(np.float32)
+    t = np.zeros(len(v), L.TRIANGLE)
+    t["v"][:, :, :3] = v
+    nodes = S.build_hlbvh(S.pack_triangles(t, np.zeros(len(v), np.int32)))
+    cam = S.parse_camera({"position": [5, 5, -20], "lookat": [5, 5, 0], "up": [0, 1, 0], "fov": 40})
+    w, h = 24, 16
+    lcv, counts = O.bvh_lcv(nodes, cam, w, h)
+    c = cam[0]
+    dist = np.float32(0.5) / np.tan(np.float32(c["arg"]) / np.float32(2))
+    n = len(v)
+    for i in range(w):
+        for j in range(h):
+            t1 = np.float32((np.float32(i) + np.float32(0.5)) / np.float32(w) - np.float32(0.5))
+            t2 = np.float32((np.float32(j) + np.float32(0.5)) / np.float32(h) - np.float32(0.5))
+            d = (dist * c["direction"][:3] + t1 * c["horizontal"][:3] + t2 * c["up"][:3]).astype(np.float32)
+            o = c["center"][:3].astype(np.float32)
+            with np.errstate(divide="ignore", invalid="ignore"):
+                def ok(k):
+                    a = (nodes[k]["bbmin"][:3] - o) / d
+                    b = (nodes[k]["bbmax"][:3] - o) / d
+                    tn, tf = np.minimum(a, b).max(), np.maximum(a, b).min()
+                    return not (tf < tn or tf < np.float32(0.001))
+                want = 0
+                for leaf in range(n - 1, 2 * n - 1):
+                    k, good = leaf, True
+                    while k != -1 and good:
+                        good = ok(k)
+                        k = nodes[k]["parent"]
+                    want += good
+            assert counts[i * h + j] == want, (i, j)
+    assert lcv == np.float32(np.sqrt((counts.astype(np.float64) ** 2).mean() - counts.mean() ** 2))
+
+
+@pytest.mark.parametrize("name", ["cbox", "mis"])
+def test_oracle_epo_vs_reference_kernel_golden(name):
+    """EPO.cl restated in C (fmaf where OpenCL contracts) against the
+    reference kernel's own per-triangle output (tests/golden/epo_*.npz,
+    tools/make_goldens.py bvh): within 1e-4 relative per triangle (the GPU's
+    3-ulp sqrt and 2.5-ulp division vs libm), the metric within 1e-6."""
+    import hashlib
+
+    from montecarlopathtracing_amd import bvhtest as B
+    path = os.path.join(GOLD, "epo_%s.npz" % name)
+    if not os.path.exists(path):
+        pytest.skip("golden not generated yet")
+    g = np.load(path)
+    d, obj = {"cbox": ("scenes/cbox/", "cbox.obj"), "mis": ("scenes/veach_mis/", "mis.obj")}[name]
+    tris = B.load_triangles(os.path.join(ROOT, d), obj)
+    for bt in ("hlbvh", "treelet"):
+        nodes = S.build_hlbvh(tris) if bt == "hlbvh" else O.treelet(S.build_hlbvh(tris))[1]
+        assert hashlib.sha1(nodes.tobytes()).digest() == g[bt + "_nodes_sha1"].tobytes()
+        e, a = O.bvh_epo(nodes, tris)
+        np.testing.assert_allclose(a, g[bt + "_area"], rtol=1e-5, atol=1e-7)
+        np.testing.assert_allclose(e, g[bt + "_epo"], rtol=1e-4, atol=1e-3 * float(np.median(g[bt + "_area"])))
+        mine = np.sum(e, dtype=np.float64) / np.sum(a, dtype=np.float64)
+        ref = np.sum(g[bt + "_epo"], dtype=np.float64) / np.sum(g[bt + "_area"], dtype=np.float64)
+        assert abs(mine - ref) <= 1e-6 * ref

@@ -116,3 +116,85 @@ def test_app_unknown_bvhtype_raises():
     app = App(C.Config(obj, configid=2), root=scenes.ROOT)
     with pytest.raises(ValueError, match="BVH Not Implemented"):
         app.init()
+
+
+# ------------------------------------------------------ testbvh metrics
+from montecarlopathtracing_amd import bvhtest as B  # noqa: E402
+
+from . import refgpu  # noqa: E402
+
+needs_ref = pytest.mark.skipif(not refgpu.available(), reason="oracle/_ref not built")
+
+METRIC_SCENES = [("cbox", "scenes/cbox/", "cbox.obj", scenes.CBOX_CAM), ("mis", "scenes/veach_mis/", "mis.obj",
+                                                                         scenes.MIS_CAM)]
+
+
+def _metric_tris(d, obj):
+    return B.load_triangles(scenes.ROOT + "/" + d, obj)
+
+
+@needs_ref
+@pytest.mark.parametrize("bvhtype", ["hlbvh", "treelet"])
+@pytest.mark.parametrize("name,d,obj,cam", METRIC_SCENES)
+def test_epo_per_triangle_bitexact_vs_reference_kernel(name, d, obj, cam, bvhtype):
+    """EPO_GPU: mcpt_bvh_epo_device's per-triangle EPO and area equal the
+    reference's EPO.cl kernel (compiled unmodified for gfx950) bit for bit."""
+    tris = _metric_tris(d, obj)
+    nodes = B.build(tris, bvhtype)
+    val, e, a, ovf = B.epo(nodes, tris, per_triangle=True)
+    re, ra = refgpu.epo(nodes, tris)
+    assert_bits_equal(a, ra, "triangle area")
+    if ovf == 0:
+        assert_bits_equal(e, re, "epo")
+    else:  # the reference overflows its points[8] there (undefined behaviour)
+        assert (e == re).mean() > 0.999
+    ref_val = np.float32(np.sum(re, dtype=np.float64) / np.sum(ra, dtype=np.float64))
+    assert np.float32(val) == ref_val
+
+
+def test_epo_random_mesh_bitexact_vs_reference_kernel():
+    if not refgpu.available():
+        pytest.skip("oracle/_ref not built")
+    tris = S.random_mesh(20_000, seed=11).tris
+    nodes = S.build_hlbvh(tris)
+    _, e, a, ovf = B.epo(nodes, tris, per_triangle=True)
+    re, ra = refgpu.epo(nodes, tris)
+    assert_bits_equal(a, ra, "triangle area")
+    assert ovf == 0
+    assert_bits_equal(e, re, "epo")
+
+
+@pytest.mark.parametrize("bvhtype", ["hlbvh", "treelet"])
+@pytest.mark.parametrize("name,d,obj,cam", METRIC_SCENES)
+def test_lcv_counts_equal_oracle(name, d, obj, cam, bvhtype):
+    """LCV: per-ray leaf counts on the GPU equal the CPU restatement of
+    bvhtest.cpp:324-444 exactly (host float semantics on both sides)."""
+    tris = _metric_tris(d, obj)
+    nodes = B.build(tris, bvhtype)
+    camera = S.parse_camera(cam)
+    w, h = 160, 120
+    v, counts = B.lcv(nodes, camera, w, h, counts=True)
+    ov, ocounts = O.bvh_lcv(nodes, camera, w, h)
+    assert (counts == ocounts).all()
+    assert np.float32(v) == np.float32(ov)
+
+
+@pytest.mark.parametrize("bvhtype", ["hlbvh", "treelet"])
+def test_sah_equals_oracle(bvhtype):
+    tris = _metric_tris("scenes/cbox/", "cbox.obj")
+    nodes = B.build(tris, bvhtype)
+    assert np.float32(B.sah(nodes)) == np.float32(O.bvh_sah(nodes))
+
+
+def test_cli_testbvh_and_testall():
+    """main.cpp:14-19 mode dispatch: config 5 (testbvh, treelet, camera) and
+    config 6 (testall) print the reference's metric lines."""
+    import subprocess
+    import sys
+    for cid, want in ((5, ("cbox.obj 33490", "treelet", "SAH: ", "EPO_GPU: ", "LCV: ")),
+                      (6, ("mis.obj 3812", "hlbvh", "SAH: ", "EPO_GPU: "))):
+        r = subprocess.run([sys.executable, "-m", "montecarlopathtracing_amd", scenes.CFG, "--configid", str(cid)],
+                           cwd=scenes.ROOT, capture_output=True, text=True, timeout=300)
+        assert r.returncode == 0, r.stderr
+        for w in want:
+            assert w in r.stdout, r.stdout

@@ -11,6 +11,7 @@
 
     python tools/make_goldens.py gpu  OUTDIR
     python tools/make_goldens.py cpu  OUTDIR
+    python tools/make_goldens.py bvh  OUTDIR   (GPU box: EPO.cl per triangle)
 """
 import ctypes
 import hashlib
@@ -86,6 +87,24 @@ def gpu(out):
     print("gpu goldens written to", out)
 
 
+def bvh(out):
+    """The reference's EPO.cl kernel (bvhtest.cpp:288-321) per triangle on the
+    cbox / veach_mis HLBVH and treelet trees (testbvh's loadObj triangles:
+    vertices only)."""
+    from montecarlopathtracing_amd import bvhtest as B
+    from tests import refgpu
+    os.makedirs(out, exist_ok=True)
+    for name, d, obj in (("cbox", "scenes/cbox/", "cbox.obj"), ("mis", "scenes/veach_mis/", "mis.obj")):
+        tris = B.load_triangles(os.path.join(ROOT, d), obj)
+        rec = {}
+        for bt in ("hlbvh", "treelet"):
+            nodes = B.build(tris, bt)
+            e, a = refgpu.epo(nodes, tris)
+            rec[bt + "_nodes_sha1"] = np.frombuffer(hashlib.sha1(nodes.tobytes()).digest(), np.uint8)
+            rec[bt + "_epo"], rec[bt + "_area"] = e, a
+        np.savez_compressed(os.path.join(out, "epo_%s.npz" % name), **rec)
+
+
 def cpu(out):
     """Reference tinyobj + stb fixtures (oracle/_ref/libref_io.so)."""
     so = ctypes.CDLL(os.path.join(ROOT, "oracle", "_ref", "libref_io.so"))
@@ -120,4 +139,4 @@ def cpu(out):
 
 if __name__ == "__main__":
     mode, out = sys.argv[1], sys.argv[2]
-    {"gpu": gpu, "cpu": cpu}[mode](out)
+    {"gpu": gpu, "cpu": cpu, "bvh": bvh}[mode](out)
