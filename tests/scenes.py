@@ -30,6 +30,12 @@ def mis():
     return S.SceneData.from_obj(os.path.join(ROOT, "scenes/veach_mis/"), "mis.obj")
 
 
+@functools.lru_cache(None)
+def dining():
+    """C4's diningroom proxy (tools/make_diningroom_proxy.py)."""
+    return S.SceneData.from_obj(os.path.join(ROOT, "scenes/diningroom/"), "diningroom.obj")
+
+
 def camera(i, w=None, h=None):
     c = dict(cfg(i).camera)
     return S.parse_camera(c)

@@ -92,7 +92,7 @@ def test_repo_config_json_parses():
 
 
 # ------------------------------------------------------------ scene loading
-@pytest.mark.parametrize("d,obj", [("cbox", "cbox.obj"), ("veach_mis", "mis.obj")])
+@pytest.mark.parametrize("d,obj", [("cbox", "cbox.obj"), ("veach_mis", "mis.obj"), ("diningroom", "diningroom.obj")])
 def test_obj_loader_matches_reference_tinyobj(d, obj):
     g = gold("tinyobj_%s.npz" % d)
     tris, mats, idx = S.load_object(os.path.join(ROOT, "scenes", d) + "/", obj)
@@ -451,3 +451,20 @@ def test_oracle_epo_vs_reference_kernel_golden(name):
         mine = np.sum(e, dtype=np.float64) / np.sum(a, dtype=np.float64)
         ref = np.sum(g[bt + "_epo"], dtype=np.float64) / np.sum(g[bt + "_area"], dtype=np.float64)
         assert abs(mine - ref) <= 1e-6 * ref
+
+
+def test_diningroom_proxy_is_regenerated_bit_for_bit(tmp_path, monkeypatch):
+    """C4's scene is a documented proxy (tools/make_diningroom_proxy.py): the
+    committed OBJ is exactly what the generator writes, with the reference's
+    diningroom.mtl materials by name and its camera in view."""
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("mkdr", os.path.join(ROOT, "tools", "make_diningroom_proxy.py"))
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    out = tmp_path / "d.obj"
+    mod.build().write(str(out))
+    assert out.read_bytes() == open(os.path.join(ROOT, "scenes", "diningroom", "diningroom.obj"), "rb").read()
+    tris, mats, idx = S.load_object(os.path.join(ROOT, "scenes", "diningroom") + "/", "diningroom.obj")
+    assert 90_000 < len(tris) < 110_000
+    assert sorted(set(mats["type"].tolist())) == [L.MCPT_DIFFUSE, L.MCPT_GLOSSY, L.MCPT_LIGHT]
+    assert (idx >= 0).all()

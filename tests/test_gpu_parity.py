@@ -54,7 +54,8 @@ def hit_fields_equal(mine, ref, live, what, check_tri=False):
         assert_bits_equal(m["triangle_id"], r["triangle_id"], what + ".triangle_id")
 
 
-SCENES = [("cbox", scenes.cbox, scenes.CBOX_CAM), ("mis", scenes.mis, scenes.MIS_CAM)]
+SCENES = [("cbox", scenes.cbox, scenes.CBOX_CAM), ("mis", scenes.mis, scenes.MIS_CAM),
+          ("dining", scenes.dining, scenes.DINING_CAM)]
 
 
 @needs_ref
@@ -141,7 +142,8 @@ def _render_both(rnd, data, camjson, w, h, depth, frames, attempt, mode=L.MODE_E
 @needs_ref
 @pytest.mark.parametrize("name,getter,camjson,depth", [("cbox", scenes.cbox, scenes.CBOX_CAM, 4),
                                                        ("cbox_diffuse", scenes.cbox_diffuse, scenes.CBOX_CAM, 8),
-                                                       ("mis", scenes.mis, scenes.MIS_CAM, 12)])
+                                                       ("mis", scenes.mis, scenes.MIS_CAM, 12),
+                                                       ("dining", scenes.dining, scenes.DINING_CAM, 16)])
 def test_render_frames_bitexact(rnd, name, getter, camjson, depth):
     (h_, c_, s_), (rh, rc, rs) = _render_both(rnd, getter(), camjson, 64, 64, depth, 6, 4)
     assert_bits_equal(c_, rc, "count")

@@ -110,7 +110,7 @@ def cpu(out):
     so = ctypes.CDLL(os.path.join(ROOT, "oracle", "_ref", "libref_io.so"))
     os.makedirs(out, exist_ok=True)
     meta = {}
-    for d, obj in (("cbox", "cbox.obj"), ("veach_mis", "mis.obj")):
+    for d, obj in (("cbox", "cbox.obj"), ("veach_mis", "mis.obj"), ("diningroom", "diningroom.obj")):
         dirp = os.path.join(ROOT, "scenes", d) + "/"
         nt, nm = ctypes.c_int64(0), ctypes.c_int32(0)
         so.ref_load_obj(dirp.encode(), obj.encode(), None, None, ctypes.byref(nt), None, ctypes.byref(nm))
