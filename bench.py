@@ -152,10 +152,18 @@ def main():
 
     ws, rank, local = dist_env()
     n = max(ws, 1)
+    # MCPT_BENCH_SHARED_GPU=1 rehearses the N-rank path on a one-GPU box: every
+    # rank on device 0, gloo for the barrier / max-reduce (tests/test_gpu_bench.py)
+    shared = os.environ.get("MCPT_BENCH_SHARED_GPU") == "1"
+    if shared:
+        local = 0
     if ws > 1:
         import torch.distributed as dist
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if shared:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     from montecarlopathtracing_amd import _lib as L
     from montecarlopathtracing_amd import render as R
     from montecarlopathtracing_amd import scene as S
@@ -189,7 +197,7 @@ def main():
     kst = rnd.stats()
     kernel_ms, launches = kst["kernel_ms"], max(kst["launches"], 1)
     if ws > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=rnd.device)
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cpu" if shared else rnd.device)
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
         elapsed = float(t.item())
 

@@ -26,6 +26,7 @@
 #include <cstring>
 #include <string>
 #include <thread>
+#include <type_traits>
 #include <vector>
 
 #include "../../include/mcpt_hip.h"
@@ -37,6 +38,7 @@ using namespace mcpt;
 #ifndef MCPT_WAVES_PER_SIMD
 #define MCPT_WAVES_PER_SIMD 4  // k_render occupancy target (tools/sweep_waves.sh)
 #endif
+constexpr int kStackWindow = 32;  // k_render's LDS window when the whole stack would cost occupancy
 
 namespace mcpt {
 int fail(int code, const std::string &msg);  // mcpt_host.cpp
@@ -115,6 +117,8 @@ struct mcpt_ctx {
   int32_t queue_cap = 0;
   int32_t *d_progress = nullptr;          // k_render per-pixel block progress
   int64_t progress_cap = 0;
+  int32_t *d_spill = nullptr;             // k_render WindowStack spill areas
+  int64_t spill_cap = 0;
   int32_t resident_blocks[2] = {0, 0};   // occupancy of k_render<EXACT|NOPRUNE> (64-thread blocks/CU)
   mcpt_stats last;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
@@ -170,21 +174,63 @@ __device__ inline void child_boxes(const DevNode &N, f3 o, f3 d, f3 rinv, BoxT &
   }
 }
 
+// Per-lane traversal stacks.  Plain: every entry in LDS, column-major
+// [depth][64] (conflict-free ds_read/write_b32).  Window: only the top K
+// entries live in LDS (entry i in slot i mod K); an entry pushed out of the
+// window goes to the lane's spill area in global memory and comes back when
+// the stack shrinks below it.  Same logical stack, so the same traversal; the
+// LDS footprint per wave drops from depth*256 B to K*256 B, which is what
+// bounds the waves per CU.
+struct PlainStack {
+  int32_t *lds;
+  int stride;
+  __device__ inline void push(int &sp, int32_t v) const { lds[(sp++) * stride] = v; }
+  __device__ inline int32_t pop(int &sp) const { return lds[(--sp) * stride]; }
+};
+template <int K>
+struct WindowStack {
+  static_assert((K & (K - 1)) == 0, "power of two window");
+  int32_t *lds;    // lds_stack + lane
+  int32_t *spill;  // this lane's entries [0, depth - K)
+  __device__ inline void push(int &sp, int32_t v) const {
+    int32_t *slot = lds + (sp & (K - 1)) * 64;
+    if (sp >= K) spill[sp - K] = *slot;
+    *slot = v;
+    ++sp;
+  }
+  __device__ inline int32_t pop(int &sp) const {
+    --sp;
+    int32_t *slot = lds + (sp & (K - 1)) * 64;
+    const int32_t v = *slot;
+    if (sp >= K) *slot = spill[sp - K];
+    return v;
+  }
+};
+
 // One 4-wide node: slab test of the 4 slots, then pick the slot to enter.
 // NEAREST (the SAH search tree): the passing slot with the smallest entry
 // distance, ties to the lower slot; otherwise (the reference tree) the lowest
 // passing slot, i.e. the reference's left-first DFS.  The other passing slots
 // are pushed so that they pop in slot order.  Returns the slot's link (an
 // internal node or ~triangle) or kPop.
-template <bool PRUNE>
-__device__ inline int32_t step4(const DevNode4 &N, f3 o, f3 rinv, float tmin, float lim, bool nearest, int32_t *stk,
-                                int &sp, int stride, uint32_t &nodes_ctr) {
-  const f4 q0 = N.q[0], q1 = N.q[1], q2 = N.q[2], q3 = N.q[3], q4 = N.q[4], q5 = N.q[5];
+template <bool PRUNE, class Stk>
+__device__ inline int32_t step4q(f4 q0, f4 q1, f4 q2, f4 q3, f4 q4, f4 q5, int32_t l0, int32_t l1, int32_t l2,
+                                 int32_t l3, f3 o, f3 rinv, float tmin, float lim, bool nearest, const Stk &stk, int &sp,
+                                 uint32_t &nodes_ctr);
+template <bool PRUNE, class Stk>
+__device__ inline int32_t step4(const DevNode4 &N, f3 o, f3 rinv, float tmin, float lim, bool nearest, const Stk &stk,
+                                int &sp, uint32_t &nodes_ctr) {
+  return step4q<PRUNE>(N.q[0], N.q[1], N.q[2], N.q[3], N.q[4], N.q[5], N.link[0], N.link[1], N.link[2], N.link[3], o,
+                       rinv, tmin, lim, nearest, stk, sp, nodes_ctr);
+}
+template <bool PRUNE, class Stk>
+__device__ inline int32_t step4q(f4 q0, f4 q1, f4 q2, f4 q3, f4 q4, f4 q5, int32_t l0, int32_t l1, int32_t l2,
+                                 int32_t l3, f3 o, f3 rinv, float tmin, float lim, bool nearest, const Stk &stk, int &sp,
+                                 uint32_t &nodes_ctr) {
   BoxT b0 = slab_pairs(q0.xy, q0.zw, q1.xy, o, rinv);
   BoxT b1 = slab_pairs(q1.zw, q2.xy, q2.zw, o, rinv);
   BoxT b2 = slab_pairs(q3.xy, q3.zw, q4.xy, o, rinv);
   BoxT b3 = slab_pairs(q4.zw, q5.xy, q5.zw, o, rinv);
-  const int32_t l0 = N.link[0], l1 = N.link[1], l2 = N.link[2], l3 = N.link[3];
   bool h0 = slab_pass(b0, tmin) && l0 != kEmptySlot, h1 = slab_pass(b1, tmin) && l1 != kEmptySlot;
   bool h2 = slab_pass(b2, tmin) && l2 != kEmptySlot, h3 = slab_pass(b3, tmin) && l3 != kEmptySlot;
   if (PRUNE) {
@@ -204,10 +250,10 @@ __device__ inline int32_t step4(const DevNode4 &N, f3 o, f3 rinv, float tmin, fl
   if (h2 && !(k2 > kb)) kb = k2, nxt = l2, sel = 2;
   if (h1 && !(k1 > kb)) kb = k1, nxt = l1, sel = 1;
   if (h0 && !(k0 > kb)) nxt = l0, sel = 0;
-  if (h3 && sel != 3) stk[(sp++) * stride] = l3;
-  if (h2 && sel != 2) stk[(sp++) * stride] = l2;
-  if (h1 && sel != 1) stk[(sp++) * stride] = l1;
-  if (h0 && sel != 0) stk[(sp++) * stride] = l0;
+  if (h3 && sel != 3) stk.push(sp, l3);
+  if (h2 && sel != 2) stk.push(sp, l2);
+  if (h1 && sel != 1) stk.push(sp, l1);
+  if (h0 && sel != 0) stk.push(sp, l0);
   return nxt;
 }
 
@@ -306,7 +352,8 @@ __device__ inline Trace traverse_exact(const SceneView &S, f3 o, f3 d, float tmi
     int sp = 0;
     while (cur != kDone) {
       while (cur >= 0) {
-        cur = step4<true>(tree[cur], o, rinv, tmin, tr.t + S.prune_margin, !ref, stk, sp, stride, tr.nodes);
+        cur = step4<true>(tree[cur], o, rinv, tmin, tr.t + S.prune_margin, !ref, PlainStack{stk, stride}, sp,
+                          tr.nodes);
         if (cur == kPop) cur = sp == 0 ? kDone : stk[(--sp) * stride];
       }
       if (cur != kDone) {
@@ -515,6 +562,8 @@ struct RenderArgs {
   uint32_t *queue;            // work-queue head (zeroed before each launch)
   int32_t lds_mats;           // 1: copy the material table to LDS after the stack
   int32_t chunk;              // queue entries a wave claims per atomic (at least)
+  int32_t *spill;             // WindowStack spill areas, one per resident lane
+  int32_t spill_stride;       // entries per lane (stack depth - window)
 };
 
 __device__ inline int32_t global_row(int32_t lr, const RenderArgs &A) {
@@ -542,13 +591,20 @@ constexpr float kTmin = 0.001f;  // host EPSILON passed as tmin (oclbasic.h:193,
 // run).  Expensive phases therefore execute with most of the wave active
 // instead of once per diverging lane.  Each lane's own
 // sequence of operations is exactly the reference's, so results are unchanged.
-template <int MODE, bool STATS>
+template <int MODE, bool STATS, bool WIN>
 __global__ void __launch_bounds__(64, MCPT_WAVES_PER_SIMD) k_render(RenderArgs A) {
   constexpr bool PRUNE = MODE != MCPT_MODE_NOPRUNE;
   constexpr bool LIT = MODE == MCPT_MODE_NOPRUNE;
   extern __shared__ int32_t lds_stack[];
   const int lane = threadIdx.x;
-  int32_t *stk = lds_stack + lane;  // column-major [depth][64]: conflict-free
+  // the whole stack in LDS, or its top kStackWindow entries (deep trees, where
+  // the whole stack would cap the resident waves per CU; chosen at launch)
+  using Stack = typename std::conditional<WIN, WindowStack<kStackWindow>, PlainStack>::type;
+  Stack stk;
+  if constexpr (WIN)
+    stk = Stack{lds_stack + lane, A.spill + ((size_t)blockIdx.x * 64 + lane) * (size_t)A.spill_stride};
+  else
+    stk = Stack{lds_stack + lane, 64};
   const SceneView &S = A.S;
   // material table copied to LDS behind the stack (small tables only)
   const mcpt_material *mats = S.mats;
@@ -685,7 +741,7 @@ __global__ void __launch_bounds__(64, MCPT_WAVES_PER_SIMD) k_render(RenderArgs A
         if (!LIT) {  // EXACT: SAH tree nearest-first, or the reference tree left-first
           uint32_t ctr = 0;
           const DevNode4 *__restrict__ tree = ref ? S.nodes4 : S.near4;
-          cur = step4<PRUNE>(tree[cur], o.xyz, rinv, kTmin, best_t + S.prune_margin, !ref, stk, sp, 64, ctr);
+          cur = step4<PRUNE>(tree[cur], o.xyz, rinv, kTmin, best_t + S.prune_margin, !ref, stk, sp, ctr);
           if (STATS) n_nodes += ctr;
         } else {  // NOPRUNE: the reference's binary tree, literal division
           const DevNode N = S.nodes[cur];
@@ -698,10 +754,10 @@ __global__ void __launch_bounds__(64, MCPT_WAVES_PER_SIMD) k_render(RenderArgs A
             hl = hl && !(bl.tnear > lim);
             hr = hr && !(br.tnear > lim);
           }
-          if (hl && hr) stk[(sp++) * 64] = N.right;  // push right, descend left
+          if (hl && hr) stk.push(sp, N.right);  // push right, descend left
           cur = hl ? N.left : (hr ? N.right : kPop);
         }
-        if (cur == kPop) cur = sp == 0 ? kDone : stk[(--sp) * 64];
+        if (cur == kPop) cur = sp == 0 ? kDone : stk.pop(sp);
       }
     }
     // ---- L: triangle tests, batched
@@ -724,7 +780,7 @@ __global__ void __launch_bounds__(64, MCPT_WAVES_PER_SIMD) k_render(RenderArgs A
             near_update(h.t, best_t, t2);
           }
         }
-        cur = sp == 0 ? kDone : stk[(--sp) * 64];
+        cur = sp == 0 ? kDone : stk.pop(sp);
       }
     }
     // ---- S: finish the segment (shade.cl), accumulate (history.cl), next segment
@@ -927,6 +983,7 @@ int mcpt_ctx_destroy(mcpt_ctx *c) {
   if (c->d_stats) (void)hipFree(c->d_stats);
   if (c->d_queue) (void)hipFree(c->d_queue);
   if (c->d_progress) (void)hipFree(c->d_progress);
+  if (c->d_spill) (void)hipFree(c->d_spill);
   if (c->ev0) (void)hipEventDestroy(c->ev0);
   if (c->ev1) (void)hipEventDestroy(c->ev1);
   delete c;
@@ -1257,9 +1314,8 @@ int mcpt_render_frames(mcpt_ctx *ctx, const mcpt_scene *scene, const mcpt_camera
   if (const char *e = std::getenv("MCPT_QUEUE_CHUNK")) A.chunk = std::max(1, std::min(4096, std::atoi(e)));  // tuning knob
   const int64_t tiles = (int64_t)A.tiles_x * ((A.local_rows + 7) / 8);
   const int depth_entries = p->mode == MCPT_MODE_NOPRUNE ? scene->stack_depth : scene->stack_depth4;
-  A.stack_depth = depth_entries;
   A.lds_mats = scene->n_mats <= 256 ? 1 : 0;
-  const size_t lds = (size_t)depth_entries * 64 * sizeof(int32_t) + (A.lds_mats ? scene->n_mats * sizeof(mcpt_material) : 0);
+  const size_t lds_mats = A.lds_mats ? scene->n_mats * sizeof(mcpt_material) : 0;
   // frames_per_launch = frames per BLOCK: a lane runs one pixel for one block
   // of frames, then hands the pixel's state to whichever lane takes its next
   // block.  One launch runs many blocks of every pixel, block-major, so lanes
@@ -1286,16 +1342,39 @@ int mcpt_render_frames(mcpt_ctx *ctx, const mcpt_scene *scene, const mcpt_camera
   }
   A.fpl = fpl;
   A.progress = ctx->d_progress;
-  // persistent grid: as many 64-lane workgroups as can be resident at once
+  // persistent grid: as many 64-lane workgroups as can be resident at once.
+  // The stack lives in LDS; when the whole stack would allow fewer resident
+  // workgroups than a kStackWindow window does, the windowed kernel runs.
   const bool noprune = p->mode == MCPT_MODE_NOPRUNE;
-  const void *kfn = noprune ? (ctx->stats_on ? (const void *)k_render<MCPT_MODE_NOPRUNE, true>
-                                             : (const void *)k_render<MCPT_MODE_NOPRUNE, false>)
-                            : (ctx->stats_on ? (const void *)k_render<MCPT_MODE_EXACT, true>
-                                             : (const void *)k_render<MCPT_MODE_EXACT, false>);
-  int per_cu = 0, n_cu = 0;
-  HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kfn, 64, lds));
+  const void *kfns[2][2][2] = {
+      {{(const void *)k_render<MCPT_MODE_EXACT, false, false>, (const void *)k_render<MCPT_MODE_EXACT, false, true>},
+       {(const void *)k_render<MCPT_MODE_EXACT, true, false>, (const void *)k_render<MCPT_MODE_EXACT, true, true>}},
+      {{(const void *)k_render<MCPT_MODE_NOPRUNE, false, false>,
+        (const void *)k_render<MCPT_MODE_NOPRUNE, false, true>},
+       {(const void *)k_render<MCPT_MODE_NOPRUNE, true, false>, (const void *)k_render<MCPT_MODE_NOPRUNE, true, true>}}};
+  const size_t lds_plain = (size_t)depth_entries * 64 * sizeof(int32_t) + lds_mats;
+  const size_t lds_win = (size_t)kStackWindow * 64 * sizeof(int32_t) + lds_mats;
+  int per_cu_plain = 0, per_cu_win = 0, n_cu = 0;
+  HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu_plain, kfns[noprune][ctx->stats_on][0], 64, lds_plain));
+  HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu_win, kfns[noprune][ctx->stats_on][1], 64, lds_win));
+  bool win = depth_entries > kStackWindow && per_cu_win > per_cu_plain;
+  if (const char *e = std::getenv("MCPT_STACK_WINDOW")) win = depth_entries > kStackWindow && std::atoi(e) != 0;  // tuning knob
+  const int per_cu = win ? per_cu_win : per_cu_plain;
+  const size_t lds = win ? lds_win : lds_plain;
+  const void *kfn = kfns[noprune][ctx->stats_on][win];
+  A.stack_depth = win ? kStackWindow : depth_entries;  // the material table follows the stack in LDS
+  A.spill_stride = win ? depth_entries - kStackWindow : 0;
   HIP_OK(hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, ctx->device));
   const int64_t grid = std::max<int64_t>(1, std::min<int64_t>(tiles, (int64_t)std::max(per_cu, 1) * n_cu));
+  const int64_t spill_need = win ? grid * 64 * (int64_t)A.spill_stride : 0;
+  if (win && spill_need > ctx->spill_cap) {
+    if (ctx->d_spill) HIP_OK(hipFree(ctx->d_spill));
+    ctx->d_spill = nullptr;
+    ctx->spill_cap = 0;
+    HIP_OK(hipMalloc(&ctx->d_spill, (size_t)spill_need * sizeof(int32_t)));
+    ctx->spill_cap = spill_need;
+  }
+  A.spill = ctx->d_spill;
   if (ctx->stats_on) HIP_OK(hipMemsetAsync(ctx->d_stats, 0, 8 * sizeof(unsigned long long), st));
   HIP_OK(hipEventRecord(ctx->ev0, st));
   int launches = 0;
@@ -1307,18 +1386,8 @@ int mcpt_render_frames(mcpt_ctx *ctx, const mcpt_scene *scene, const mcpt_camera
       A.blocks = (A.frames + fpl - 1) / fpl;
       A.queue = ctx->d_queue + launches;
       if (A.blocks > 1) HIP_OK(hipMemsetAsync(ctx->d_progress, 0, (size_t)n_px * sizeof(int32_t), st));
-      if (noprune) {
-        if (ctx->stats_on)
-          hipLaunchKernelGGL((k_render<MCPT_MODE_NOPRUNE, true>), dim3(grid), dim3(64), lds, st, A);
-        else
-          hipLaunchKernelGGL((k_render<MCPT_MODE_NOPRUNE, false>), dim3(grid), dim3(64), lds, st, A);
-      } else {
-        if (ctx->stats_on)
-          hipLaunchKernelGGL((k_render<MCPT_MODE_EXACT, true>), dim3(grid), dim3(64), lds, st, A);
-        else
-          hipLaunchKernelGGL((k_render<MCPT_MODE_EXACT, false>), dim3(grid), dim3(64), lds, st, A);
-      }
-      HIP_OK(hipGetLastError());
+      void *kargs[] = {&A};
+      HIP_OK(hipLaunchKernel(kfn, dim3(grid), dim3(64), kargs, lds, st));
       ++launches;
     }
   }

@@ -247,3 +247,17 @@ def test_frame_blocks_handoff_full_size(rnd):
         for a, b, what in zip(outs[0], o, ("hist", "count", "seeds")):
             assert_bits_equal(a, b, what)
     dsc.close()
+
+
+@needs_ref
+@pytest.mark.parametrize("name,getter,camjson,depth", [("cbox", scenes.cbox, scenes.CBOX_CAM, 8),
+                                                       ("dining", scenes.dining, scenes.DINING_CAM, 16)])
+def test_render_windowed_stack_bitexact(rnd, monkeypatch, name, getter, camjson, depth):
+    """The LDS-window stack (top 32 entries in LDS, the rest spilled to a
+    per-lane global area; picked at launch for deep trees) is the same
+    logical stack: forced on, renders still match the reference bit for bit."""
+    monkeypatch.setenv("MCPT_STACK_WINDOW", "1")
+    (h_, c_, s_), (rh, rc, rs) = _render_both(rnd, getter(), camjson, 64, 64, depth, 4, 4)
+    assert_bits_equal(c_, rc, "count")
+    assert_bits_equal(s_, rs, "seeds")
+    assert_bits_equal(h_, rh, "hist")
