@@ -1359,8 +1359,13 @@ int mcpt_render_frames(mcpt_ctx *ctx, const mcpt_scene *scene, const mcpt_camera
   HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu_win, kfns[noprune][ctx->stats_on][1], 64, lds_win));
   bool win = depth_entries > kStackWindow && per_cu_win > per_cu_plain;
   if (const char *e = std::getenv("MCPT_STACK_WINDOW")) win = depth_entries > kStackWindow && std::atoi(e) != 0;  // tuning knob
-  const int per_cu = win ? per_cu_win : per_cu_plain;
-  const size_t lds = win ? lds_win : lds_plain;
+  const int per_cu_any = win ? per_cu_win : per_cu_plain;
+  size_t lds = win ? lds_win : lds_plain;
+  int per_cu = per_cu_any;
+  if (const char *e = std::getenv("MCPT_LDS_PAD")) {  // tuning knob: occupancy experiments (extra LDS per workgroup)
+    lds += (size_t)std::max(0, std::atoi(e));
+    HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kfns[noprune][ctx->stats_on][win], 64, lds));
+  }
   const void *kfn = kfns[noprune][ctx->stats_on][win];
   A.stack_depth = win ? kStackWindow : depth_entries;  // the material table follows the stack in LDS
   A.spill_stride = win ? depth_entries - kStackWindow : 0;

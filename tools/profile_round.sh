@@ -10,13 +10,14 @@ R=$PWD
 O=$R/gpurun_out/prof_$TAG
 mkdir -p $O
 export TMPDIR=/tmp
-timeout -k 10 400 python bench.py --workload $WL > $O/bench.json 2> $O/bench.err || { echo "bench failed"; tail $O/bench.err; exit 1; }
+STEPS=${STEPS:-64}
+timeout -k 10 400 python bench.py --workload $WL --steps $STEPS > $O/bench.json 2> $O/bench.err || { echo "bench failed"; tail $O/bench.err; exit 1; }
 cat $O/bench.json
 cd /tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/trace -- \
-  python3 $R/bench.py --no-cpu --workload $WL --steps 64 --warmup 64 > $O/trace.log 2>&1 || { echo "trace failed"; tail $O/trace.log; exit 1; }
+  python3 $R/bench.py --no-cpu --workload $WL --steps $STEPS --warmup $STEPS > $O/trace.log 2>&1 || { echo "trace failed"; tail $O/trace.log; exit 1; }
 for c in FETCH_SIZE WRITE_SIZE; do
   timeout -k 10 300 rocprofv3 --pmc $c --output-format csv -d $O/pmc_$c -- \
-    python3 $R/bench.py --no-cpu --workload $WL --steps 64 --warmup 64 > $O/pmc_$c.log 2>&1 || { echo "pmc $c failed"; tail $O/pmc_$c.log; exit 1; }
+    python3 $R/bench.py --no-cpu --workload $WL --steps $STEPS --warmup $STEPS > $O/pmc_$c.log 2>&1 || { echo "pmc $c failed"; tail $O/pmc_$c.log; exit 1; }
 done
 echo profile done

@@ -27,7 +27,7 @@ def one(pattern):
 
 def main():
     tag = sys.argv[1] if len(sys.argv) > 1 else "r01"
-    kernel = sys.argv[2] if len(sys.argv) > 2 else "k_render<0, false>"
+    kernel = sys.argv[2] if len(sys.argv) > 2 else "k_render<0, false, "  # EXACT, no stats, either stack
     src = os.path.join(ROOT, "gpurun_out", "prof_" + tag)
     dst = os.path.join(ROOT, "profiles")
     shutil.copy(os.path.join(src, "bench.json"), os.path.join(dst, tag + "_bench.json"))
@@ -45,7 +45,8 @@ def main():
     bench = json.loads(open(os.path.join(dst, tag + "_bench.json")).read().strip().splitlines()[-1])
     rd = per["FETCH_SIZE"][0] * 1024 * 2
     wr = per["WRITE_SIZE"][0] * 1024
-    out = {"workload": "bench.py --no-cpu --steps 64 --warmup 64 (" + bench["config"]["workload"] + "), 64 frames per launch in blocks of 16",
+    out = {"workload": "bench.py --no-cpu --steps %d --warmup %d (%s), %d frames per launch in blocks of 16" % (
+               bench["steps"], bench["steps"], bench["config"]["workload"], bench["steps"]),
            "kernel": kernel, "launches_averaged": per["FETCH_SIZE"][1],
            "FETCH_SIZE_kB_per_launch": per["FETCH_SIZE"][0], "WRITE_SIZE_kB_per_launch": per["WRITE_SIZE"][0],
            "hbm_read_bytes_per_launch_corrected": rd, "hbm_write_bytes_per_launch": wr,
