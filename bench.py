@@ -145,6 +145,8 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--frames-per-launch", type=int, default=16)
     ap.add_argument("--workload", default="C2", choices=sorted(WORKLOADS))
+    ap.add_argument("--schedule", default="auto", choices=["auto", "single", "paired"],
+                    help="k_render leaf-test schedule; auto times both before the warmup (untimed)")
     args = ap.parse_args()
     global W, H_PER_GPU, DEPTH
     wl = WORKLOADS[args.workload]
@@ -178,6 +180,11 @@ def main():
     st = rnd.new_state(W, h_img, seeds)
     kw = dict(stripe_rows=STRIPE_ROWS, stripe_index=rank, stripe_count=n, frames_per_launch=args.frames_per_launch)
     attempt = 1 << 30  # accumulate every frame (the reference's MAX_ATTEMPT cap never binds here)
+    # leaf-test schedule (identical images; speed only), chosen before any timing
+    if args.schedule == "auto":
+        rnd.tune_schedule(dsc, cam, st, DEPTH, attempt, frames=args.frames_per_launch, **kw)
+    else:
+        dsc.schedule = L.SCHED_PAIRED if args.schedule == "paired" else L.SCHED_SINGLE
 
     # warmup (untimed)
     if args.warmup > 0:
@@ -254,7 +261,8 @@ def main():
                                               if args.workload == "C2" else "see config.workload"),
                "config": {"workload": wl["desc"],
                           "width": W, "height_per_gpu": h_img // n if strong else H_PER_GPU, "max_depth": DEPTH,
-                          "parallelism": "row-stripe tiles x%d" % n, "mode": "exact"},
+                          "parallelism": "row-stripe tiles x%d" % n, "mode": "exact",
+                          "schedule": "paired" if dsc.schedule == L.SCHED_PAIRED else "single"},
                "active_Msegments_per_s": round(segments * n / elapsed / 1e6, 2),
                "roofline": roof, "cpu_baseline": cpu}
         print(json.dumps(out), flush=True)

@@ -123,8 +123,17 @@ typedef struct mcpt_render_params {
   int32_t mode;                     /* MCPT_MODE_*                          */
   int32_t frames_per_launch;        /* frames per block (a lane runs one pixel
                                        for one block, then hands it on); 0 = 16 */
-  int32_t reserved;
+  int32_t schedule;                 /* MCPT_SCHED_*: how k_render batches leaf
+                                       tests (results identical; speed only) */
 } mcpt_render_params;
+
+/* Leaf-test schedules of the fused kernel (bit-identical results):
+ *  MCPT_SCHED_SINGLE — one triangle per lane per leaf phase (default; C2)
+ *  MCPT_SCHED_PAIRED — a lane whose next stack entry is also a leaf tests
+ *                      both in one phase (faster on C3/C4-like scenes);
+ *  Renderer.tune_schedule() picks one by timing both. */
+#define MCPT_SCHED_SINGLE 0
+#define MCPT_SCHED_PAIRED 1
 
 typedef struct mcpt_stats {
   uint64_t segments;                /* rays alive at intersect entry, all frames */

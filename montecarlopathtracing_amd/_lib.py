@@ -30,13 +30,14 @@ for _dt, _sz in ((CAMERA, 80), (RAY, 48), (HIT, 48), (TRIANGLE, 64), (MATERIAL, 
 
 MCPT_DIFFUSE, MCPT_GLOSSY, MCPT_TRANSPARENT, MCPT_LIGHT = 1, 2, 3, 4
 MODE_EXACT, MODE_NOPRUNE = 0, 1
+SCHED_SINGLE, SCHED_PAIRED = 0, 1  # mcpt_render_params.schedule
 TERMINATED = 0xFF000000
 
 
 class RenderParams(ctypes.Structure):
     _fields_ = [(n, ctypes.c_int32) for n in (
         "width", "height", "max_depth", "max_attempt", "frame_begin", "frames", "stripe_rows",
-        "stripe_index", "stripe_count", "mode", "frames_per_launch", "reserved")]
+        "stripe_index", "stripe_count", "mode", "frames_per_launch", "schedule")]
 
 
 class Stats(ctypes.Structure):

@@ -71,6 +71,9 @@ class App:
             self.init()
         att = self.cfg.MAXATTEPMT()
         todo = frames
+        if frames >= 256 and not getattr(self, "_tuned", False):  # long runs: time both leaf schedules first
+            self.renderer.tune_schedule(self.scene, self.camera, self.state, self.cfg.MAXDEPTH(), att)
+            self._tuned = True
         while todo > 0:
             n = todo if self.attempt_count > att else min(todo, att + 1 - self.attempt_count)
             self.renderer.render_frames(self.scene, self.camera, self.state, self.cfg.MAXDEPTH(), att, n)

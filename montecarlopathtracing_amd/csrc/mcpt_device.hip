@@ -186,6 +186,7 @@ struct PlainStack {
   int stride;
   __device__ inline void push(int &sp, int32_t v) const { lds[(sp++) * stride] = v; }
   __device__ inline int32_t pop(int &sp) const { return lds[(--sp) * stride]; }
+  __device__ inline int32_t peek(int sp) const { return lds[(sp - 1) * stride]; }
 };
 template <int K>
 struct WindowStack {
@@ -205,6 +206,7 @@ struct WindowStack {
     if (sp >= K) *slot = spill[sp - K];
     return v;
   }
+  __device__ inline int32_t peek(int sp) const { return lds[((sp - 1) & (K - 1)) * 64]; }  // the top is in the window
 };
 
 // One 4-wide node: slab test of the 4 slots, then pick the slot to enter.
@@ -591,7 +593,7 @@ constexpr float kTmin = 0.001f;  // host EPSILON passed as tmin (oclbasic.h:193,
 // run).  Expensive phases therefore execute with most of the wave active
 // instead of once per diverging lane.  Each lane's own
 // sequence of operations is exactly the reference's, so results are unchanged.
-template <int MODE, bool STATS, bool WIN>
+template <int MODE, bool STATS, bool WIN, bool PAIR>
 __global__ void __launch_bounds__(64, MCPT_WAVES_PER_SIMD) k_render(RenderArgs A) {
   constexpr bool PRUNE = MODE != MCPT_MODE_NOPRUNE;
   constexpr bool LIT = MODE == MCPT_MODE_NOPRUNE;
@@ -766,19 +768,32 @@ __global__ void __launch_bounds__(64, MCPT_WAVES_PER_SIMD) k_render(RenderArgs A
     if (ml && (__popcll(ml) >= A.th_leaf || !__ballot(live && cur >= 0))) {
       if (STATS && lane == __builtin_ctzll(__ballot(1))) w_l++;
       if (in_l) {
-        const int32_t id = ~cur;
-        const DevTri T = S.tris[id];
-        TriHit h = LIT ? cramer(d.xyz, T.nab.xyz, T.nac.xyz, T.v0.xyz - o.xyz, T.nrm.xyz, kTmin)
-                       : cramer_reduced(d.xyz, T.nab.xyz, T.nac.xyz, T.v0.xyz - o.xyz, T.nrm.xyz, T.v0.w,
-                                        T.nab.w, T.nac.w, kTmin);
-        if (STATS) n_tests++;
-        if (h.accept) {
-          if (ref ? best_t - h.t >= kEps : h.t < best_t) best_nrm = T.nrm;  // objdef.h:213
-          if (ref) {
-            if (best_t - h.t >= kEps) best_t = h.t;
-          } else {
-            near_update(h.t, best_t, t2);
+        // PAIR (MCPT_SCHED_PAIRED): when the next stack entry is a leaf too,
+        // its triangle is fetched with this one and tested right after it;
+        // the lane's sequence of tests is unchanged, one phase serves two leaves
+        const int32_t nx = !PAIR || sp == 0 ? kDone : stk.peek(sp);
+        const bool two = PAIR && nx < 0 && nx != kDone;
+        const DevTri T = S.tris[~cur];
+        DevTri T2;
+        if (two) T2 = S.tris[~nx];
+        auto test = [&](const DevTri &X) {
+          TriHit h = LIT ? cramer(d.xyz, X.nab.xyz, X.nac.xyz, X.v0.xyz - o.xyz, X.nrm.xyz, kTmin)
+                         : cramer_reduced(d.xyz, X.nab.xyz, X.nac.xyz, X.v0.xyz - o.xyz, X.nrm.xyz, X.v0.w,
+                                          X.nab.w, X.nac.w, kTmin);
+          if (STATS) n_tests++;
+          if (h.accept) {
+            if (ref ? best_t - h.t >= kEps : h.t < best_t) best_nrm = X.nrm;  // objdef.h:213
+            if (ref) {
+              if (best_t - h.t >= kEps) best_t = h.t;
+            } else {
+              near_update(h.t, best_t, t2);
+            }
           }
+        };
+        test(T);
+        if (two) {
+          (void)stk.pop(sp);
+          test(T2);
         }
         cur = sp == 0 ? kDone : stk.pop(sp);
       }
@@ -1273,6 +1288,8 @@ static int check_render(const mcpt_render_params *p) {
       (int64_t)p->width * p->height > (int64_t)INT32_MAX)
     return mcpt::fail(MCPT_ERR_ARG, "render: bad parameters");
   if (p->mode != MCPT_MODE_EXACT && p->mode != MCPT_MODE_NOPRUNE) return mcpt::fail(MCPT_ERR_ARG, "render: bad mode");
+  if (p->schedule != MCPT_SCHED_SINGLE && p->schedule != MCPT_SCHED_PAIRED)
+    return mcpt::fail(MCPT_ERR_ARG, "render: bad schedule");
   return MCPT_OK;
 }
 
@@ -1304,7 +1321,10 @@ int mcpt_render_frames(mcpt_ctx *ctx, const mcpt_scene *scene, const mcpt_camera
   A.max_depth = p->max_depth;
   A.max_attempt = p->max_attempt;
   A.stack_depth = scene->stack_depth;
-  A.th_leaf = 4;  // tuned on C2 (tools/sweep_env.sh): leaf phase at >= 4 lanes, shade at >= 32
+  // tuned (tools/sweep_env.sh, tools/gpu_thr.sh): leaf phase at >= 4 lanes
+  // (single-leaf schedule, C2) or >= 12 (paired, C3/C4), shade at >= 32
+  const bool pair = p->schedule == MCPT_SCHED_PAIRED;
+  A.th_leaf = pair ? 12 : 4;
   A.th_shade = 32;
   if (const char *e = std::getenv("MCPT_PHASE_THRESHOLDS")) {  // tuning knob: "leaf,shade"
     int a = 0, b = 0;
@@ -1346,17 +1366,19 @@ int mcpt_render_frames(mcpt_ctx *ctx, const mcpt_scene *scene, const mcpt_camera
   // The stack lives in LDS; when the whole stack would allow fewer resident
   // workgroups than a kStackWindow window does, the windowed kernel runs.
   const bool noprune = p->mode == MCPT_MODE_NOPRUNE;
-  const void *kfns[2][2][2] = {
-      {{(const void *)k_render<MCPT_MODE_EXACT, false, false>, (const void *)k_render<MCPT_MODE_EXACT, false, true>},
-       {(const void *)k_render<MCPT_MODE_EXACT, true, false>, (const void *)k_render<MCPT_MODE_EXACT, true, true>}},
-      {{(const void *)k_render<MCPT_MODE_NOPRUNE, false, false>,
-        (const void *)k_render<MCPT_MODE_NOPRUNE, false, true>},
-       {(const void *)k_render<MCPT_MODE_NOPRUNE, true, false>, (const void *)k_render<MCPT_MODE_NOPRUNE, true, true>}}};
+  // [noprune][stats][window][pair]
+#define MCPT_KR(M, ST, W) {(const void *)k_render<M, ST, W, false>, (const void *)k_render<M, ST, W, true>}
+  const void *kfns[2][2][2][2] = {
+      {{MCPT_KR(MCPT_MODE_EXACT, false, false), MCPT_KR(MCPT_MODE_EXACT, false, true)},
+       {MCPT_KR(MCPT_MODE_EXACT, true, false), MCPT_KR(MCPT_MODE_EXACT, true, true)}},
+      {{MCPT_KR(MCPT_MODE_NOPRUNE, false, false), MCPT_KR(MCPT_MODE_NOPRUNE, false, true)},
+       {MCPT_KR(MCPT_MODE_NOPRUNE, true, false), MCPT_KR(MCPT_MODE_NOPRUNE, true, true)}}};
+#undef MCPT_KR
   const size_t lds_plain = (size_t)depth_entries * 64 * sizeof(int32_t) + lds_mats;
   const size_t lds_win = (size_t)kStackWindow * 64 * sizeof(int32_t) + lds_mats;
   int per_cu_plain = 0, per_cu_win = 0, n_cu = 0;
-  HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu_plain, kfns[noprune][ctx->stats_on][0], 64, lds_plain));
-  HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu_win, kfns[noprune][ctx->stats_on][1], 64, lds_win));
+  HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu_plain, kfns[noprune][ctx->stats_on][0][pair], 64, lds_plain));
+  HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu_win, kfns[noprune][ctx->stats_on][1][pair], 64, lds_win));
   bool win = depth_entries > kStackWindow && per_cu_win > per_cu_plain;
   if (const char *e = std::getenv("MCPT_STACK_WINDOW")) win = depth_entries > kStackWindow && std::atoi(e) != 0;  // tuning knob
   const int per_cu_any = win ? per_cu_win : per_cu_plain;
@@ -1364,9 +1386,9 @@ int mcpt_render_frames(mcpt_ctx *ctx, const mcpt_scene *scene, const mcpt_camera
   int per_cu = per_cu_any;
   if (const char *e = std::getenv("MCPT_LDS_PAD")) {  // tuning knob: occupancy experiments (extra LDS per workgroup)
     lds += (size_t)std::max(0, std::atoi(e));
-    HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kfns[noprune][ctx->stats_on][win], 64, lds));
+    HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kfns[noprune][ctx->stats_on][win][pair], 64, lds));
   }
-  const void *kfn = kfns[noprune][ctx->stats_on][win];
+  const void *kfn = kfns[noprune][ctx->stats_on][win][pair];
   A.stack_depth = win ? kStackWindow : depth_entries;  // the material table follows the stack in LDS
   A.spill_stride = win ? depth_entries - kStackWindow : 0;
   HIP_OK(hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, ctx->device));

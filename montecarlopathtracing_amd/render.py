@@ -46,6 +46,7 @@ class DeviceScene:
         self.renderer = renderer
         self.data = data
         self.handle = ctypes.c_void_p()
+        self.schedule = L.SCHED_SINGLE  # k_render leaf-test schedule (Renderer.tune_schedule)
         t = np.ascontiguousarray(data.tris)
         nd = np.ascontiguousarray(data.nodes)
         m = np.ascontiguousarray(data.mats)
@@ -111,6 +112,7 @@ class Renderer:
 
     def set_stats(self, on):
         L.check(L.lib().mcpt_set_stats(self.ctx, int(bool(on))))
+        self._stats_on = bool(on)
 
     def stats(self):
         s = L.Stats()
@@ -138,9 +140,10 @@ class Renderer:
     # ---------------------------------------------------------- fused path
     def render_frames(self, scene, camera, state, max_depth, max_attempt, frames, frame_begin=None,
                       stripe_rows=16, stripe_index=0, stripe_count=1, mode=L.MODE_EXACT,
-                      frames_per_launch=0):
+                      frames_per_launch=0, schedule=None):
         """Frames [frame_begin, frame_begin+frames) for this GPU's row stripes
-        (OpenCL::update x frames + ColorOut accumulation)."""
+        (OpenCL::update x frames + ColorOut accumulation).  `schedule`
+        (L.SCHED_*; default: the scene's, see tune_schedule) only changes speed."""
         p = L.RenderParams()
         p.width, p.height = state.width, state.height
         p.max_depth, p.max_attempt = int(max_depth), int(max_attempt)
@@ -149,11 +152,33 @@ class Renderer:
         p.stripe_rows, p.stripe_index, p.stripe_count = int(stripe_rows), int(stripe_index), int(stripe_count)
         p.mode = int(mode)
         p.frames_per_launch = int(frames_per_launch)
+        p.schedule = int(getattr(scene, "schedule", L.SCHED_SINGLE) if schedule is None else schedule)
         cam = np.ascontiguousarray(camera)
         L.check(L.lib().mcpt_render_frames(self.ctx, scene.handle, L.ptr(cam), ctypes.byref(p), L.ptr(state.seeds),
                                            L.ptr(state.hist), L.ptr(state.count), _stream()))
         state.frames_done = p.frame_begin + p.frames
         return state
+
+    def tune_schedule(self, scene, camera, state, max_depth, max_attempt, frames=16, trials=2, **kw):
+        """Pick the faster leaf-test schedule for this scene and view: render
+        `frames` frames `trials` times with each schedule on a scratch copy
+        of `state` (interleaved, device time of each call), keep the faster
+        in scene.schedule.  Both schedules give bit-identical images, so this
+        only moves speed.  Returns (schedule, {schedule: best ms})."""
+        if getattr(self, "_stats_on", False):
+            raise L.MCPTError("tune_schedule: counters must be off (they change the kernel)")
+        scratch = ImageState.__new__(ImageState)
+        scratch.width, scratch.height, scratch.frames_done = state.width, state.height, state.frames_done
+        best = {}
+        for _ in range(int(trials)):
+            for sched in (L.SCHED_SINGLE, L.SCHED_PAIRED):
+                scratch.seeds, scratch.hist, scratch.count = state.seeds.clone(), state.hist.clone(), state.count.clone()
+                self.render_frames(scene, camera, scratch, max_depth, max_attempt, frames,
+                                   frame_begin=state.frames_done, schedule=sched, **kw)
+                ms = self.stats()["kernel_ms"]
+                best[sched] = min(best.get(sched, ms), ms)
+        scene.schedule = min(best, key=lambda k: (best[k], k))
+        return scene.schedule, best
 
     # ------------------------------------------------ wavefront (drop-in)
     def generate_rays(self, camera, width, height):

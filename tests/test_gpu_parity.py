@@ -144,8 +144,9 @@ def _render_both(rnd, data, camjson, w, h, depth, frames, attempt, mode=L.MODE_E
                                                        ("cbox_diffuse", scenes.cbox_diffuse, scenes.CBOX_CAM, 8),
                                                        ("mis", scenes.mis, scenes.MIS_CAM, 12),
                                                        ("dining", scenes.dining, scenes.DINING_CAM, 16)])
-def test_render_frames_bitexact(rnd, name, getter, camjson, depth):
-    (h_, c_, s_), (rh, rc, rs) = _render_both(rnd, getter(), camjson, 64, 64, depth, 6, 4)
+@pytest.mark.parametrize("schedule", [L.SCHED_SINGLE, L.SCHED_PAIRED])
+def test_render_frames_bitexact(rnd, name, getter, camjson, depth, schedule):
+    (h_, c_, s_), (rh, rc, rs) = _render_both(rnd, getter(), camjson, 64, 64, depth, 6, 4, schedule=schedule)
     assert_bits_equal(c_, rc, "count")
     assert_bits_equal(s_, rs, "seeds")
     assert_bits_equal(h_, rh, "hist")
@@ -252,12 +253,59 @@ def test_frame_blocks_handoff_full_size(rnd):
 @needs_ref
 @pytest.mark.parametrize("name,getter,camjson,depth", [("cbox", scenes.cbox, scenes.CBOX_CAM, 8),
                                                        ("dining", scenes.dining, scenes.DINING_CAM, 16)])
-def test_render_windowed_stack_bitexact(rnd, monkeypatch, name, getter, camjson, depth):
+@pytest.mark.parametrize("schedule", [L.SCHED_SINGLE, L.SCHED_PAIRED])
+def test_render_windowed_stack_bitexact(rnd, monkeypatch, name, getter, camjson, depth, schedule):
     """The LDS-window stack (top 32 entries in LDS, the rest spilled to a
     per-lane global area; picked at launch for deep trees) is the same
     logical stack: forced on, renders still match the reference bit for bit."""
     monkeypatch.setenv("MCPT_STACK_WINDOW", "1")
-    (h_, c_, s_), (rh, rc, rs) = _render_both(rnd, getter(), camjson, 64, 64, depth, 4, 4)
+    (h_, c_, s_), (rh, rc, rs) = _render_both(rnd, getter(), camjson, 64, 64, depth, 4, 4, schedule=schedule)
     assert_bits_equal(c_, rc, "count")
     assert_bits_equal(s_, rs, "seeds")
     assert_bits_equal(h_, rh, "hist")
+
+
+@pytest.mark.parametrize("mode", [L.MODE_EXACT, L.MODE_NOPRUNE])
+def test_paired_schedule_equals_single_full_size(rnd, mode):
+    """Size-independent property at the C2 and C3 configurations: the paired
+    leaf-test schedule (MCPT_SCHED_PAIRED) changes only speed, never bits."""
+    for getter, camjson, depth, w in ((scenes.cbox_diffuse, scenes.CBOX_CAM, 8, 512),
+                                      (scenes.mis, scenes.MIS_CAM, 12, 384)):
+        data, cam = getter(), S.parse_camera(camjson)
+        seeds = R.default_seeds(w * w)
+        dsc = rnd.upload(data)
+        outs = []
+        for sched in (L.SCHED_SINGLE, L.SCHED_PAIRED):
+            st = rnd.new_state(w, w, seeds)
+            rnd.render_frames(dsc, cam, st, depth, 1 << 20, 8, mode=mode, schedule=sched)
+            torch.cuda.synchronize()
+            outs.append((st.hist.cpu().numpy(), st.count.cpu().numpy(), st.seeds_np()))
+        for a, b, what in zip(outs[0], outs[1], ("hist", "count", "seeds")):
+            assert_bits_equal(a, b, what)
+        dsc.close()
+
+
+def test_tune_schedule_leaves_state_alone(rnd):
+    """Renderer.tune_schedule renders on a scratch copy: the caller's state is
+    untouched, the scene keeps a valid schedule, and rendering afterwards
+    gives the untuned bits."""
+    data, cam = scenes.mis(), S.parse_camera(scenes.MIS_CAM)
+    w = h = 128
+    seeds = R.default_seeds(w * h)
+    dsc = rnd.upload(data)
+    ref = rnd.new_state(w, h, seeds)
+    rnd.render_frames(dsc, cam, ref, 12, 1 << 20, 6, schedule=L.SCHED_SINGLE)
+    st = rnd.new_state(w, h, seeds)
+    sched, best = rnd.tune_schedule(dsc, cam, st, 12, 1 << 20, frames=4, trials=1)
+    assert sched in (L.SCHED_SINGLE, L.SCHED_PAIRED) and dsc.schedule == sched
+    assert set(best) == {L.SCHED_SINGLE, L.SCHED_PAIRED} and all(v > 0 for v in best.values())
+    assert st.frames_done == 0 and int(st.count.sum()) == 0 and float(st.hist.abs().sum()) == 0.0
+    assert_bits_equal(st.seeds_np(), seeds.astype(np.uint32), "seeds untouched")
+    rnd.render_frames(dsc, cam, st, 12, 1 << 20, 6)
+    torch.cuda.synchronize()
+    for a, b, what in zip((st.hist.cpu().numpy(), st.count.cpu().numpy(), st.seeds_np()),
+                          (ref.hist.cpu().numpy(), ref.count.cpu().numpy(), ref.seeds_np()), ("hist", "count", "seeds")):
+        assert_bits_equal(a, b, what)
+    with pytest.raises(L.MCPTError):
+        rnd.render_frames(dsc, cam, st, 12, 1 << 20, 1, schedule=7)
+    dsc.close()
