@@ -233,7 +233,7 @@ def main():
                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                     "B_seg": round(b_seg, 1), "E_node": round(ec["E_node"], 3), "E_tri": round(ec["E_tri"], 3),
                     "segments_per_launch": int(seg_per_launch), "avg_launch_ms": round(avg_launch_s * 1e3, 3),
-                    "kernel": "k_render<0,false>",
+                    "kernel": "k_render<EXACT, no stats, %s>" % ("paired" if dsc.schedule == L.SCHED_PAIRED else "single"),
                     "kernel_node_fetches_per_seg": round(cst["node_visits"] / max(segments, 1), 3),
                     "kernel_tri_tests_per_seg": round(cst["tri_tests"] / max(segments, 1), 3)}
             # the records this kernel itself gathers per segment (128-B 4-wide

@@ -1322,9 +1322,9 @@ int mcpt_render_frames(mcpt_ctx *ctx, const mcpt_scene *scene, const mcpt_camera
   A.max_attempt = p->max_attempt;
   A.stack_depth = scene->stack_depth;
   // tuned (tools/sweep_env.sh, tools/gpu_thr.sh): leaf phase at >= 4 lanes
-  // (single-leaf schedule, C2) or >= 12 (paired, C3/C4), shade at >= 32
+  // (single-leaf schedule) or >= 16 (paired), shade at >= 32
   const bool pair = p->schedule == MCPT_SCHED_PAIRED;
-  A.th_leaf = pair ? 12 : 4;
+  A.th_leaf = pair ? 16 : 4;
   A.th_shade = 32;
   if (const char *e = std::getenv("MCPT_PHASE_THRESHOLDS")) {  // tuning knob: "leaf,shade"
     int a = 0, b = 0;
