@@ -19,10 +19,10 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def one(pattern):
-    hits = sorted(glob.glob(pattern))
+    hits = sorted(glob.glob(pattern), key=os.path.getmtime)
     if not hits:
         raise SystemExit("missing: " + pattern)
-    return hits[-1]
+    return hits[-1]  # the newest run
 
 
 def main():
