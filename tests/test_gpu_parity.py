@@ -309,3 +309,38 @@ def test_tune_schedule_leaves_state_alone(rnd):
     with pytest.raises(L.MCPTError):
         rnd.render_frames(dsc, cam, st, 12, 1 << 20, 1, schedule=7)
     dsc.close()
+
+
+@needs_ref
+@pytest.mark.parametrize("w,h,depth,frames,attempt", [(1, 1, 4, 5, 4), (7, 3, 6, 9, 2), (65, 33, 3, 4, 0),
+                                                      (130, 9, 1, 3, 8)])
+@pytest.mark.parametrize("schedule", [L.SCHED_SINGLE, L.SCHED_PAIRED])
+def test_render_edge_sizes_bitexact(rnd, w, h, depth, frames, attempt, schedule):
+    """Ragged and tiny images (edge tiles with holes, a 1x1 image), depth 1,
+    and the MAX_ATTEMPT cap at 0 (history never runs) match the reference."""
+    (h_, c_, s_), (rh, rc, rs) = _render_both(rnd, scenes.cbox(), scenes.CBOX_CAM, w, h, depth, frames, attempt,
+                                              schedule=schedule, frames_per_launch=2)
+    assert_bits_equal(c_, rc, "count")
+    assert_bits_equal(s_, rs, "seeds")
+    assert_bits_equal(h_, rh, "hist")
+
+
+def test_render_zero_frames_and_bad_params(rnd):
+    """frames = 0 is a no-op; malformed parameters are status errors."""
+    data, cam = scenes.cbox(), S.parse_camera(scenes.CBOX_CAM)
+    w = h = 16
+    seeds = R.default_seeds(w * h)
+    dsc = rnd.upload(data)
+    st = rnd.new_state(w, h, seeds)
+    rnd.render_frames(dsc, cam, st, 4, 4, 0)
+    torch.cuda.synchronize()
+    assert int(st.count.sum()) == 0 and float(st.hist.abs().sum()) == 0.0
+    assert_bits_equal(st.seeds_np(), seeds.astype(np.uint32), "seeds")
+    for kw in (dict(stripe_index=2, stripe_count=2), dict(stripe_rows=0), dict(mode=5)):
+        with pytest.raises(L.MCPTError):
+            rnd.render_frames(dsc, cam, st, 4, 4, 1, **kw)
+    with pytest.raises(L.MCPTError):
+        rnd.render_frames(dsc, cam, st, 0, 4, 1)  # max_depth must be >= 1
+    with pytest.raises(L.MCPTError):
+        rnd.render_frames(dsc, cam, st, 4, 4, -1)
+    dsc.close()
