@@ -58,8 +58,10 @@ def render_distributed(renderer, scene, camera, width, height, max_depth, max_at
     Returns (hist, count, seeds) as numpy on rank 0, None elsewhere."""
     rank, world = dist.get_rank(group), dist.get_world_size(group)
     st = renderer.new_state(width, height, seeds)
-    renderer.render_frames(scene, camera, st, max_depth, max_attempt, frames, stripe_rows=stripe_rows,
-                           stripe_index=rank, stripe_count=world, mode=mode)
+    kw = dict(stripe_rows=stripe_rows, stripe_index=rank, stripe_count=world, mode=mode)
+    if frames >= 256:  # long runs: each rank picks the faster leaf-test schedule (same bits either way)
+        renderer.tune_schedule(scene, camera, st, max_depth, max_attempt, **kw)
+    renderer.render_frames(scene, camera, st, max_depth, max_attempt, frames, **kw)
     torch.cuda.synchronize()
     mask = ownership_mask(width, height, stripe_rows, rank, world)
     h, c, s = reduce_image(st.hist, st.count, st.seeds, mask, group=group)
