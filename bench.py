@@ -143,7 +143,8 @@ def main():
     ap.add_argument("--steps", type=int, default=64)
     ap.add_argument("--warmup", type=int, default=4)
     ap.add_argument("--no-cpu", action="store_true")
-    ap.add_argument("--frames-per-launch", type=int, default=16)
+    ap.add_argument("--frames-per-launch", type=int, default=0,
+                    help="frames per pixel block; 0 = the library's load-balance choice (4..16)")
     ap.add_argument("--workload", default="C2", choices=sorted(WORKLOADS))
     ap.add_argument("--schedule", default="auto", choices=["auto", "single", "paired"],
                     help="k_render leaf-test schedule; auto times both before the warmup (untimed)")
@@ -182,7 +183,7 @@ def main():
     attempt = 1 << 30  # accumulate every frame (the reference's MAX_ATTEMPT cap never binds here)
     # leaf-test schedule (identical images; speed only), chosen before any timing
     if args.schedule == "auto":
-        rnd.tune_schedule(dsc, cam, st, DEPTH, attempt, frames=args.frames_per_launch, **kw)
+        rnd.tune_schedule(dsc, cam, st, DEPTH, attempt, frames=16, **kw)
     else:
         dsc.schedule = L.SCHED_PAIRED if args.schedule == "paired" else L.SCHED_SINGLE
 
@@ -203,6 +204,7 @@ def main():
     elapsed = time.perf_counter() - t0
     kst = rnd.stats()
     kernel_ms, launches = kst["kernel_ms"], max(kst["launches"], 1)
+    fpb = kst["frames_per_block"]
     if ws > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device="cpu" if shared else rnd.device)
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
@@ -262,7 +264,8 @@ def main():
                "config": {"workload": wl["desc"],
                           "width": W, "height_per_gpu": h_img // n if strong else H_PER_GPU, "max_depth": DEPTH,
                           "parallelism": "row-stripe tiles x%d" % n, "mode": "exact",
-                          "schedule": "paired" if dsc.schedule == L.SCHED_PAIRED else "single"},
+                          "schedule": "paired" if dsc.schedule == L.SCHED_PAIRED else "single",
+                          "frames_per_block": fpb},
                "active_Msegments_per_s": round(segments * n / elapsed / 1e6, 2),
                "roofline": roof, "cpu_baseline": cpu}
         print(json.dumps(out), flush=True)

@@ -122,7 +122,8 @@ typedef struct mcpt_render_params {
   int32_t stripe_count;             /* number of GPUs (1 = whole image)     */
   int32_t mode;                     /* MCPT_MODE_*                          */
   int32_t frames_per_launch;        /* frames per block (a lane runs one pixel
-                                       for one block, then hands it on); 0 = 16 */
+                                       for one block, then hands it on);
+                                       <= 0: auto, 4..16 by load balance */
   int32_t schedule;                 /* MCPT_SCHED_*: how k_render batches leaf
                                        tests (results identical; speed only) */
 } mcpt_render_params;
@@ -142,7 +143,7 @@ typedef struct mcpt_stats {
   uint64_t bad_material;            /* hits on an unknown material type      */
   double   kernel_ms;               /* device time of the last render call   */
   int32_t  launches;                /* kernel launches of the last render call */
-  int32_t  pad;
+  int32_t  frames_per_block;        /* block size the last render call used   */
   uint64_t wave_node_phases;        /* wave-level node steps (SIMT efficiency = */
   uint64_t wave_leaf_phases;        /*  node_visits / (64 * wave_node_phases)) */
   uint64_t wave_shade_phases;

@@ -43,7 +43,7 @@ class RenderParams(ctypes.Structure):
 class Stats(ctypes.Structure):
     _fields_ = [("segments", ctypes.c_uint64), ("node_visits", ctypes.c_uint64),
                 ("tri_tests", ctypes.c_uint64), ("bad_material", ctypes.c_uint64),
-                ("kernel_ms", ctypes.c_double), ("launches", ctypes.c_int32), ("pad", ctypes.c_int32),
+                ("kernel_ms", ctypes.c_double), ("launches", ctypes.c_int32), ("frames_per_block", ctypes.c_int32),
                 ("wave_node_phases", ctypes.c_uint64), ("wave_leaf_phases", ctypes.c_uint64),
                 ("wave_shade_phases", ctypes.c_uint64), ("order_fallbacks", ctypes.c_uint64)]
 

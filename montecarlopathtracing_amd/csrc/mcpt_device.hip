@@ -1336,32 +1336,6 @@ int mcpt_render_frames(mcpt_ctx *ctx, const mcpt_scene *scene, const mcpt_camera
   const int depth_entries = p->mode == MCPT_MODE_NOPRUNE ? scene->stack_depth : scene->stack_depth4;
   A.lds_mats = scene->n_mats <= 256 ? 1 : 0;
   const size_t lds_mats = A.lds_mats ? scene->n_mats * sizeof(mcpt_material) : 0;
-  // frames_per_launch = frames per BLOCK: a lane runs one pixel for one block
-  // of frames, then hands the pixel's state to whichever lane takes its next
-  // block.  One launch runs many blocks of every pixel, block-major, so lanes
-  // stay busy until the last block (no per-block drain of the GPU).
-  const int fpl = p->frames_per_launch > 0 ? p->frames_per_launch : 16;
-  const uint32_t n_items = (uint32_t)A.tiles_x * (uint32_t)((A.local_rows + 7) / 8) * 64u;
-  const int64_t max_blocks = std::max<int64_t>(1, std::min<int64_t>(INT32_MAX / std::max<uint32_t>(n_items, 1), 4096 / fpl + 1));
-  const int64_t n_blocks_all = (p->frames + fpl - 1) / fpl;
-  const int n_launch = (int)((n_blocks_all + max_blocks - 1) / max_blocks);
-  if (n_launch > ctx->queue_cap) {  // one queue head per launch, zeroed by a single memset
-    if (ctx->d_queue) HIP_OK(hipFree(ctx->d_queue));
-    ctx->d_queue = nullptr;
-    ctx->queue_cap = 0;
-    HIP_OK(hipMalloc(&ctx->d_queue, (size_t)std::max(n_launch, 64) * sizeof(uint32_t)));
-    ctx->queue_cap = std::max(n_launch, 64);
-  }
-  const int64_t n_px = (int64_t)p->width * p->height;
-  if (n_blocks_all > 1 && n_px > ctx->progress_cap) {
-    if (ctx->d_progress) HIP_OK(hipFree(ctx->d_progress));
-    ctx->d_progress = nullptr;
-    ctx->progress_cap = 0;
-    HIP_OK(hipMalloc(&ctx->d_progress, (size_t)n_px * sizeof(int32_t)));
-    ctx->progress_cap = n_px;
-  }
-  A.fpl = fpl;
-  A.progress = ctx->d_progress;
   // persistent grid: as many 64-lane workgroups as can be resident at once.
   // The stack lives in LDS; when the whole stack would allow fewer resident
   // workgroups than a kStackWindow window does, the windowed kernel runs.
@@ -1401,6 +1375,41 @@ int mcpt_render_frames(mcpt_ctx *ctx, const mcpt_scene *scene, const mcpt_camera
     HIP_OK(hipMalloc(&ctx->d_spill, (size_t)spill_need * sizeof(int32_t)));
     ctx->spill_cap = spill_need;
   }
+  // frames_per_launch = frames per BLOCK: a lane runs one pixel for one block
+  // of frames, then hands the pixel's state to whichever lane takes its next
+  // block.  One launch runs many blocks of every pixel, block-major, so lanes
+  // stay busy until the last block (no per-block drain of the GPU).
+  // frames_per_launch <= 0: auto — blocks of 16 frames unless that leaves
+  // fewer than 16 queue entries per resident lane (short calls, strong-scaled
+  // ranks: load balance), then 8 or 4.  Smaller blocks on big calls lost on
+  // scenes with short paths (C3: 33.8 vs 56.3 G samples/s at 8 frames).
+  const uint32_t n_items = (uint32_t)A.tiles_x * (uint32_t)((A.local_rows + 7) / 8) * 64u;
+  int fpl = p->frames_per_launch;
+  if (fpl <= 0) {
+    const double per_lane = (double)n_items * std::max(p->frames, 1) / (double)(grid * 64);
+    fpl = 16;
+    while (fpl > 4 && per_lane / fpl < 16.0) fpl /= 2;
+  }
+  const int64_t max_blocks = std::max<int64_t>(1, std::min<int64_t>(INT32_MAX / std::max<uint32_t>(n_items, 1), 4096 / fpl + 1));
+  const int64_t n_blocks_all = (p->frames + fpl - 1) / fpl;
+  const int n_launch = (int)((n_blocks_all + max_blocks - 1) / max_blocks);
+  if (n_launch > ctx->queue_cap) {  // one queue head per launch, zeroed by a single memset
+    if (ctx->d_queue) HIP_OK(hipFree(ctx->d_queue));
+    ctx->d_queue = nullptr;
+    ctx->queue_cap = 0;
+    HIP_OK(hipMalloc(&ctx->d_queue, (size_t)std::max(n_launch, 64) * sizeof(uint32_t)));
+    ctx->queue_cap = std::max(n_launch, 64);
+  }
+  const int64_t n_px = (int64_t)p->width * p->height;
+  if (n_blocks_all > 1 && n_px > ctx->progress_cap) {
+    if (ctx->d_progress) HIP_OK(hipFree(ctx->d_progress));
+    ctx->d_progress = nullptr;
+    ctx->progress_cap = 0;
+    HIP_OK(hipMalloc(&ctx->d_progress, (size_t)n_px * sizeof(int32_t)));
+    ctx->progress_cap = n_px;
+  }
+  A.fpl = fpl;
+  A.progress = ctx->d_progress;
   A.spill = ctx->d_spill;
   if (ctx->stats_on) HIP_OK(hipMemsetAsync(ctx->d_stats, 0, 8 * sizeof(unsigned long long), st));
   HIP_OK(hipEventRecord(ctx->ev0, st));
@@ -1425,6 +1434,7 @@ int mcpt_render_frames(mcpt_ctx *ctx, const mcpt_scene *scene, const mcpt_camera
   std::memset(&ctx->last, 0, sizeof(ctx->last));
   ctx->last.kernel_ms = ms;
   ctx->last.launches = launches;
+  ctx->last.frames_per_block = fpl;
   if (ctx->stats_on) {
     unsigned long long h[8];
     HIP_OK(hipMemcpy(h, ctx->d_stats, sizeof(h), hipMemcpyDeviceToHost));

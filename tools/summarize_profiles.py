@@ -45,8 +45,9 @@ def main():
     bench = json.loads(open(os.path.join(dst, tag + "_bench.json")).read().strip().splitlines()[-1])
     rd = per["FETCH_SIZE"][0] * 1024 * 2
     wr = per["WRITE_SIZE"][0] * 1024
-    out = {"workload": "bench.py --no-cpu --steps %d --warmup %d (%s), %d frames per launch in blocks of 16" % (
-               bench["steps"], bench["steps"], bench["config"]["workload"], bench["steps"]),
+    out = {"workload": "bench.py --no-cpu --steps %d --warmup %d (%s), %d frames per launch in blocks of %d" % (
+               bench["steps"], bench["steps"], bench["config"]["workload"], bench["steps"],
+               bench["config"].get("frames_per_block", 16)),
            "kernel": kernel, "launches_averaged": per["FETCH_SIZE"][1],
            "FETCH_SIZE_kB_per_launch": per["FETCH_SIZE"][0], "WRITE_SIZE_kB_per_launch": per["WRITE_SIZE"][0],
            "hbm_read_bytes_per_launch_corrected": rd, "hbm_write_bytes_per_launch": wr,
