@@ -219,6 +219,24 @@ def main():
     rnd.set_stats(False)
     segments = cst["segments"]
 
+    # the job's one exchange, after the timed frames: every rank's row stripes
+    # summed onto rank 0 (dist.reduce_image: RCCL over xGMI; gloo when rehearsed
+    # on a shared GPU), timed on its own and reported beside the frame rate
+    reduce_ms = None
+    if ws > 1:
+        from montecarlopathtracing_amd import dist as D
+        mask = D.ownership_mask(W, h_img, STRIPE_ROWS, rank, n)
+        bufs = (st.hist, st.count, st.seeds)
+        if shared:  # gloo: host copies
+            bufs = tuple(b.cpu() for b in bufs)
+        torch.cuda.synchronize()
+        torch.distributed.barrier()
+        t1 = time.perf_counter()
+        D.reduce_image(*bufs, mask)
+        torch.cuda.synchronize()
+        torch.distributed.barrier()
+        reduce_ms = (time.perf_counter() - t1) * 1e3
+
     total_samples = float(W * h_img) * args.steps * DEPTH
     value = total_samples / elapsed / 1e6
     out = None
@@ -267,6 +285,7 @@ def main():
                           "schedule": "paired" if dsc.schedule == L.SCHED_PAIRED else "single",
                           "frames_per_block": fpb},
                "active_Msegments_per_s": round(segments * n / elapsed / 1e6, 2),
+               "image_reduce_ms": None if reduce_ms is None else round(reduce_ms, 3),
                "roofline": roof, "cpu_baseline": cpu}
         print(json.dumps(out), flush=True)
     dsc.close()

@@ -41,6 +41,7 @@ def test_bench_two_ranks_rehearsal():
     assert j["n_gpus"] == 2 and j["steps"] == 4 and j["scaling"] == "weak"
     assert j["value"] > 0 and j["config"]["parallelism"] == "row-stripe tiles x2"
     assert j["cpu_baseline"] is None  # rank 0 at N=1 only
+    assert j["image_reduce_ms"] is not None and j["image_reduce_ms"] > 0  # the final image reduce ran
 
 
 def test_bench_c4_strong_two_ranks_rehearsal():
@@ -52,3 +53,4 @@ def test_bench_c4_strong_two_ranks_rehearsal():
     assert r.returncode == 0, r.stderr[-3000:]
     j = _lines(r.stdout)[0]
     assert j["scaling"] == "strong" and j["config"]["height_per_gpu"] == 540
+    assert j["image_reduce_ms"] is not None
