@@ -183,7 +183,8 @@ def main():
     attempt = 1 << 30  # accumulate every frame (the reference's MAX_ATTEMPT cap never binds here)
     # leaf-test schedule (identical images; speed only), chosen before any timing
     if args.schedule == "auto":
-        rnd.tune_schedule(dsc, cam, st, DEPTH, attempt, frames=16, **kw)
+        # timed on calls of the timed call's size (same frame-block regime), 3 trials each
+        rnd.tune_schedule(dsc, cam, st, DEPTH, attempt, frames=max(1, min(args.steps, 64)), trials=3, **kw)
     else:
         dsc.schedule = L.SCHED_PAIRED if args.schedule == "paired" else L.SCHED_SINGLE
 
