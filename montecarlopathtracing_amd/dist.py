@@ -43,6 +43,8 @@ def reduce_image(hist, count, seeds, mask, group=None, dst=0):
     hist (N,4) float32, count (N,) int32, seeds (N,) int32 view of u32 — any
     device the process group's backend supports.  Non-owned pixels are zeroed
     before the reduce, so the sum is exact (one contributor per pixel)."""
+    if hist.is_cuda and dist.get_backend(group) == "gloo":  # gloo reduces host tensors
+        hist, count, seeds = hist.cpu(), count.cpu(), seeds.cpu()
     m = torch.as_tensor(mask, device=hist.device)
     h = torch.where(m[:, None], hist, torch.zeros_like(hist))
     c = torch.where(m, count, torch.zeros_like(count))
