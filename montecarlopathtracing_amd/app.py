@@ -71,7 +71,7 @@ class App:
             self.init()
         att = self.cfg.MAXATTEPMT()
         todo = frames
-        if frames >= 256 and not getattr(self, "_tuned", False):  # long runs: time both leaf schedules first
+        if frames >= 4096 and not getattr(self, "_tuned", False):  # long runs (tuning costs 128 frames): time both leaf schedules
             self.renderer.tune_schedule(self.scene, self.camera, self.state, self.cfg.MAXDEPTH(), att)
             self._tuned = True
         while todo > 0:

@@ -46,7 +46,7 @@ class DeviceScene:
         self.renderer = renderer
         self.data = data
         self.handle = ctypes.c_void_p()
-        self.schedule = L.SCHED_SINGLE  # k_render leaf-test schedule (Renderer.tune_schedule)
+        self.schedule = L.SCHED_PAIRED  # k_render leaf-test schedule: paired measured faster on C2-C5 (tune_schedule)
         t = np.ascontiguousarray(data.tris)
         nd = np.ascontiguousarray(data.nodes)
         m = np.ascontiguousarray(data.mats)
@@ -152,14 +152,14 @@ class Renderer:
         p.stripe_rows, p.stripe_index, p.stripe_count = int(stripe_rows), int(stripe_index), int(stripe_count)
         p.mode = int(mode)
         p.frames_per_launch = int(frames_per_launch)
-        p.schedule = int(getattr(scene, "schedule", L.SCHED_SINGLE) if schedule is None else schedule)
+        p.schedule = int(getattr(scene, "schedule", L.SCHED_PAIRED) if schedule is None else schedule)
         cam = np.ascontiguousarray(camera)
         L.check(L.lib().mcpt_render_frames(self.ctx, scene.handle, L.ptr(cam), ctypes.byref(p), L.ptr(state.seeds),
                                            L.ptr(state.hist), L.ptr(state.count), _stream()))
         state.frames_done = p.frame_begin + p.frames
         return state
 
-    def tune_schedule(self, scene, camera, state, max_depth, max_attempt, frames=16, trials=2, **kw):
+    def tune_schedule(self, scene, camera, state, max_depth, max_attempt, frames=64, trials=1, **kw):
         """Pick the faster leaf-test schedule for this scene and view: render
         `frames` frames `trials` times with each schedule on a scratch copy
         of `state` (interleaved, device time of each call), keep the faster
