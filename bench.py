@@ -6,23 +6,31 @@ fused HIP path-tracing loop on BASELINE.json configs[1] (C2): Scene/cbox,
     python bench.py [--gpus N] [--steps K] [--warmup W]
     torchrun --nproc-per-node N ... bench.py --gpus N       (one process per GPU)
 
-A step = one frame: every pixel of the rank's image tile traces one sample of
-up to 8 bounces and is accumulated (OpenCL::update + ColorOut once).  Scaling
-is weak: each rank owns a 1024x1024 tile of a 1024 x (1024*N) image (row
-stripes interleaved across ranks); no collective runs inside the timed region.
-The timed region is bracketed by barrier + synchronize and the max over ranks
-is reported.  Scene data, seeds and accumulators are resident in HBM before
-timing starts.
+A step = one frame: every pixel of the image traces one sample of up to 8
+bounces and is accumulated (OpenCL::update + ColorOut once).  At N > 1 the
+headline is strong scaling, as north_star asks ("tile-parallel scaling of
+1024x1024 renders"): the fixed 1024x1024 image is split into 16-row stripes
+dealt round-robin to the ranks; the weak-scaled rate (each rank a 1024x1024
+tile of a 1024 x 1024N image) is timed after it and reported under
+"weak_scaling".  No collective runs inside the timed region.  The timed region
+is bracketed by barrier + synchronize and the max over ranks is reported.
+Scene data, seeds and accumulators are resident in HBM before timing starts.
 
-Also reported (rank 0, N=1 only for cpu_baseline):
-  roofline     — SURVEY.md §8(d): algorithmic bytes per active segment
-                 B_seg = 328 + 64 (E_node + E_tri), E_* measured per config by
-                 the CPU oracle's t-pruned left-first traversal (cached in
-                 profiles/e_counts.json); achieved = B_seg x segments per launch
-                 / average launch time (HIP events on the launch stream).
+Also reported (rank 0; cpu_baseline at N=1 only):
+  roofline     — the hot kernel k_render against HBM.  traffic = memory-side
+                 bytes per launch (rocprofv3 FETCH_SIZE x the calibrated scale
+                 + WRITE_SIZE, the timed launch of this same command, committed
+                 in profiles/pmc_summary.json by tools/profile.py); achieved =
+                 traffic / the launch's device time measured here (HIP events
+                 on the launch stream); frac = achieved / 8 TB/s.  issue_frac =
+                 the VALU-busy fraction of the same profile (the ceiling that
+                 binds the cache-resident scenes), with the L1/L2 hit rates.
+                 ref_traversal_equiv_GBps restates the rate in SURVEY.md
+                 §8(d)'s B_seg units (bytes the reference's traversal would
+                 move per segment); it is not HBM traffic.
   cpu_baseline — the CPU oracle (plain-C restatement of the reference
-                 algorithm, OpenMP) on a bounded pixel sample of the same
-                 workload, on this host's cores.
+                 algorithm, OpenMP on every core this process may use) on a
+                 bounded pixel sample of the same workload.
 """
 import argparse
 import json
@@ -39,13 +47,13 @@ import torch  # noqa: E402
 STRIPE_ROWS = 16
 # BASELINE.json configs: the headline is C2; C3/C5 are extra bench lines (--workload)
 WORKLOADS = {
-    "C2": {"desc": "C2: cbox 1024x1024/GPU, 8 bounces, diffuse-only, 1 sample/pixel/step",
+    "C2": {"desc": "C2: cbox 1024x1024, 8 bounces, diffuse-only, 1 sample/pixel/step",
            "w": 1024, "h": 1024, "depth": 8},
-    "C3": {"desc": "C3: veach_mis 1024x1024/GPU, 12 bounces, glossy+emitters, 1 sample/pixel/step",
+    "C3": {"desc": "C3: veach_mis 1024x1024, 12 bounces, glossy+emitters, 1 sample/pixel/step",
            "w": 1024, "h": 1024, "depth": 12},
-    "C4": {"desc": "C4: diningroom proxy 1920x1080 (whole image over all GPUs), 16 bounces, glossy, "
-                   "1 sample/pixel/step", "w": 1920, "h": 1080, "depth": 16, "strong": True},
-    "C5": {"desc": "C5: 10M random triangles, 2048x2048/GPU, 8 bounces, 1 sample/pixel/step",
+    "C4": {"desc": "C4: diningroom proxy 1920x1080, 16 bounces, glossy, 1 sample/pixel/step",
+           "w": 1920, "h": 1080, "depth": 16, "strong": True},
+    "C5": {"desc": "C5: 10M random triangles, 2048x2048, 8 bounces, 1 sample/pixel/step",
            "w": 2048, "h": 2048, "depth": 8},
 }
 W, H_PER_GPU, DEPTH = 1024, 1024, 8
@@ -78,7 +86,8 @@ def load_scene(workload):
         d = S.SceneData.from_obj(os.path.join(ROOT, "scenes/diningroom/"), "diningroom.obj")
         return d.with_nodes(R.treelet_device(d.nodes)), DINING_CAM
     if workload == "C5":
-        return S.random_mesh(10_000_000), S.RANDOM_MESH_CAMERA
+        from montecarlopathtracing_amd import render as R  # the HLBVH built on the GPU (same tree as the host's)
+        return S.random_mesh(10_000_000, build=R.build_hlbvh_host_nodes), S.RANDOM_MESH_CAMERA
     raise ValueError(workload)
 
 
@@ -98,13 +107,28 @@ def default_seeds(n):
     return ds(n)
 
 
+def cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
 def cpu_baseline(data, cam, h_img, target_s=15.0):
     """The CPU oracle on a bounded sample: every k-th pixel of the same image,
-    same depth, frames scaled so the sample takes ~target_s seconds."""
+    same depth, frames scaled so the sample takes ~target_s seconds, on every
+    core this process may run on (all host cores)."""
     from tests import oracle as O
     if not O.available():
         return None
-    threads = max(1, min(16, os.cpu_count() or 1))
+    try:
+        threads = len(os.sched_getaffinity(0))
+    except AttributeError:
+        threads = os.cpu_count() or 1
+    threads = max(1, threads)
     seeds = default_seeds(W * h_img)
     stride = 61
     px = np.arange(0, W * h_img, stride, dtype=np.int32)
@@ -117,24 +141,46 @@ def cpu_baseline(data, cam, h_img, target_s=15.0):
     _, _, _, st = O.render(data, cam, W, h_img, DEPTH, frames, 1 << 20, seeds, pixels=px, threads=threads)
     dt = time.time() - t0
     return {"value": len(px) * frames * DEPTH / dt / 1e6, "unit": "Msamples/s", "cores": threads,
-            "kind": "port",
+            "kind": "port", "nproc": os.cpu_count(), "cpu_model": cpu_model(), "threads": threads,
             "sample": "every %dth pixel (%d px) of the 1024x1024 C2 image x %d frames x depth %d, %.1f s; "
                       "oracle/mcpt_oracle.c exhaustive reference traversal, %d OpenMP threads" % (
                           stride, len(px), frames, DEPTH, dt, threads),
             "active_Msegments_per_s": float(st[0]) / dt / 1e6}
 
 
-def load_traffic(workload, steps):
-    """Memory-side bytes per launch of the hot kernel from the committed
-    rocprofv3 PMC summary (tools/summarize_profiles.py), for this workload
-    and launch size only; None otherwise."""
+def load_profile(workload, steps):
+    """The committed rocprofv3 summary of the timed launch of THIS command
+    (workload, frames per call), written by tools/profile.py; None if that
+    exact launch size was never profiled."""
     path = os.path.join(ROOT, "profiles", "pmc_summary.json")
     try:
         with open(path) as fh:
-            j = json.load(fh).get(workload) or {}
+            return json.load(fh).get("%s@%d" % (workload, steps))
     except (OSError, ValueError):
         return None
-    return j.get("hbm_bytes_per_launch") if j.get("frames_per_launch") == steps else None
+
+
+def timed_render(rnd, dsc, cam, st, steps, warmup, kw, ws, shared):
+    """W untimed warmup frames, then K frames timed between barrier +
+    synchronize on both sides; returns (elapsed s, max over ranks)."""
+    attempt = 1 << 30  # accumulate every frame (the reference's MAX_ATTEMPT cap never binds here)
+    if warmup > 0:
+        rnd.render_frames(dsc, cam, st, DEPTH, attempt, warmup, **kw)
+    torch.cuda.synchronize()
+    if ws > 1:
+        torch.distributed.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    rnd.render_frames(dsc, cam, st, DEPTH, attempt, steps, **kw)
+    torch.cuda.synchronize()
+    if ws > 1:
+        torch.distributed.barrier()
+    elapsed = time.perf_counter() - t0
+    if ws > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cpu" if shared else rnd.device)
+        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+        elapsed = float(t.item())
+    return elapsed
 
 
 def main():
@@ -144,10 +190,11 @@ def main():
     ap.add_argument("--warmup", type=int, default=4)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--frames-per-launch", type=int, default=0,
-                    help="frames per pixel block; 0 = the library's load-balance choice (4..16)")
+                    help="frames per pixel block; 0 = the library's load-balance choice")
     ap.add_argument("--workload", default="C2", choices=sorted(WORKLOADS))
     ap.add_argument("--schedule", default="auto", choices=["auto", "single", "paired"],
                     help="k_render leaf-test schedule; auto times both before the warmup (untimed)")
+    ap.add_argument("--no-weak", action="store_true", help="N > 1: skip the weak-scaling leg")
     args = ap.parse_args()
     global W, H_PER_GPU, DEPTH
     wl = WORKLOADS[args.workload]
@@ -171,8 +218,8 @@ def main():
     from montecarlopathtracing_amd import render as R
     from montecarlopathtracing_amd import scene as S
 
-    strong = bool(wl.get("strong"))
-    h_img = H_PER_GPU if strong else H_PER_GPU * n  # strong: one fixed image striped over the ranks
+    # strong scaling: one fixed image striped over the ranks (the headline)
+    h_img = H_PER_GPU
     data, camj = load_scene(args.workload)
     cam = S.parse_camera(camj)
     rnd = R.Renderer(local if ws > 1 else 0)
@@ -180,7 +227,7 @@ def main():
     seeds = default_seeds(W * h_img)
     st = rnd.new_state(W, h_img, seeds)
     kw = dict(stripe_rows=STRIPE_ROWS, stripe_index=rank, stripe_count=n, frames_per_launch=args.frames_per_launch)
-    attempt = 1 << 30  # accumulate every frame (the reference's MAX_ATTEMPT cap never binds here)
+    attempt = 1 << 30
     # leaf-test schedule (identical images; speed only), chosen before any timing
     if args.schedule == "auto":
         # timed on calls of the timed call's size (same frame-block regime), 3 trials each
@@ -188,42 +235,27 @@ def main():
     else:
         dsc.schedule = L.SCHED_PAIRED if args.schedule == "paired" else L.SCHED_SINGLE
 
-    # warmup (untimed)
-    if args.warmup > 0:
-        rnd.render_frames(dsc, cam, st, DEPTH, attempt, args.warmup, **kw)
-    # snapshot for the segment-count replay
-    snap = (st.seeds.clone(), st.hist.clone(), st.count.clone(), st.frames_done)
-    torch.cuda.synchronize()
-    if ws > 1:
-        torch.distributed.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    rnd.render_frames(dsc, cam, st, DEPTH, attempt, args.steps, **kw)
-    torch.cuda.synchronize()
-    if ws > 1:
-        torch.distributed.barrier()
-    elapsed = time.perf_counter() - t0
+    elapsed = timed_render(rnd, dsc, cam, st, args.steps, args.warmup, kw, ws, shared)
     kst = rnd.stats()
     kernel_ms, launches = kst["kernel_ms"], max(kst["launches"], 1)
     fpb = kst["frames_per_block"]
-    if ws > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device="cpu" if shared else rnd.device)
-        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
-        elapsed = float(t.item())
 
     # replay the same frames with counters on (deterministic: same segments)
-    st.seeds.copy_(snap[0]), st.hist.copy_(snap[1]), st.count.copy_(snap[2])
-    st.frames_done = snap[3]
+    st2 = rnd.new_state(W, h_img, seeds)
+    if args.warmup > 0:
+        rnd.render_frames(dsc, cam, st2, DEPTH, attempt, args.warmup, **kw)
     rnd.set_stats(True)
-    rnd.render_frames(dsc, cam, st, DEPTH, attempt, args.steps, **kw)
+    rnd.render_frames(dsc, cam, st2, DEPTH, attempt, args.steps, **kw)
     cst = rnd.stats()
     rnd.set_stats(False)
     segments = cst["segments"]
+    del st2
 
     # the job's one exchange, after the timed frames: every rank's row stripes
     # summed onto rank 0 (dist.reduce_image: RCCL over xGMI; gloo when rehearsed
     # on a shared GPU), timed on its own and reported beside the frame rate
     reduce_ms = None
+    weak = None
     if ws > 1:
         from montecarlopathtracing_amd import dist as D
         mask = D.ownership_mask(W, h_img, STRIPE_ROWS, rank, n)
@@ -237,56 +269,66 @@ def main():
         torch.cuda.synchronize()
         torch.distributed.barrier()
         reduce_ms = (time.perf_counter() - t1) * 1e3
+        if not args.no_weak and not wl.get("strong"):
+            # weak scaling: a 1024 x 1024N image, each rank a 1024x1024 share
+            h_weak = H_PER_GPU * n
+            stw = rnd.new_state(W, h_weak, default_seeds(W * h_weak))
+            ew = timed_render(rnd, dsc, cam, stw, args.steps, args.warmup, kw, ws, shared)
+            weak = {"value": round(float(W * h_weak) * args.steps * DEPTH / ew / 1e6, 2), "unit": "Msamples/s",
+                    "ms_per_step": round(ew * 1e3 / args.steps, 4), "image": [W, h_weak],
+                    "note": "each rank renders a 1024x1024 share of a 1024 x 1024N image"}
+            del stw
 
     total_samples = float(W * h_img) * args.steps * DEPTH
     value = total_samples / elapsed / 1e6
     out = None
     if rank == 0:
+        avg_launch_s = kernel_ms / 1e3 / launches
+        seg_per_launch = segments / float(launches)
+        prof = load_profile(args.workload, args.steps) if n == 1 else None
+        roof = {"bound": "hbm", "peak": HBM_PEAK_GBS, "unit": "GB/s", "achieved": None, "frac": None, "traffic": None,
+                "kernel": "k_render<EXACT, no stats, %s>" % ("paired" if dsc.schedule == L.SCHED_PAIRED else "single"),
+                "avg_launch_ms": round(avg_launch_s * 1e3, 3), "segments_per_launch": int(seg_per_launch),
+                "kernel_node_fetches_per_seg": round(cst["node_visits"] / max(segments, 1), 3),
+                "kernel_tri_tests_per_seg": round(cst["tri_tests"] / max(segments, 1), 3)}
+        if prof:
+            traffic = prof["hbm_bytes_per_launch"]
+            roof["traffic"] = traffic
+            roof["achieved"] = round(traffic / avg_launch_s / 1e9, 2)
+            roof["frac"] = round(roof["achieved"] / HBM_PEAK_GBS, 5)
+            roof["issue_frac"] = prof.get("valu_busy")
+            roof["binding"] = "gather latency + VALU issue (cache-resident scene; see DESIGN.md §3.6)"
+            for k in ("l1_hit_rate", "l2_hit_rate", "l2_hit_GBps_128B_lines", "wave_wait_any_per_wave_cycle",
+                      "gather_latency_cycles_per_vmem_rd", "fetch_scale_calibrated", "timed_launch_ms_rocprof"):
+                roof[k] = prof.get(k)
+            roof["profile"] = prof.get("source")
         ec = e_counts(args.workload)
-        roof = None
         if ec:
             b_seg = 328.0 + 64.0 * (ec["E_node"] + ec["E_tri"])
-            seg_per_launch = segments / float(launches)
-            avg_launch_s = kernel_ms / 1e3 / launches
-            achieved = b_seg * seg_per_launch / avg_launch_s / 1e9
-            traffic = load_traffic(args.workload, args.steps)
-            roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                    "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                    "B_seg": round(b_seg, 1), "E_node": round(ec["E_node"], 3), "E_tri": round(ec["E_tri"], 3),
-                    "segments_per_launch": int(seg_per_launch), "avg_launch_ms": round(avg_launch_s * 1e3, 3),
-                    "kernel": "k_render<EXACT, no stats, %s>" % ("paired" if dsc.schedule == L.SCHED_PAIRED else "single"),
-                    "kernel_node_fetches_per_seg": round(cst["node_visits"] / max(segments, 1), 3),
-                    "kernel_tri_tests_per_seg": round(cst["tri_tests"] / max(segments, 1), 3)}
-            # the records this kernel itself gathers per segment (128-B 4-wide
-            # nodes, 64-B triangles, 48 B of pixel state per pixel-launch):
-            # frac > 1 above means the kernel needs fewer bytes than the
-            # reference traversal's B_seg, not that it beats HBM
-            own = (128.0 * cst["node_visits"] + 64.0 * cst["tri_tests"]
-                   + 48.0 * W * h_img / n * max(cst["launches"], 1)) / max(segments, 1)
-            roof["own_bytes_per_seg"] = round(own, 1)
-            roof["own_achieved"] = round(own * seg_per_launch / avg_launch_s / 1e9, 1)
-            roof["own_frac"] = round(roof["own_achieved"] / HBM_PEAK_GBS, 4)
-            # the measured streaming-read bandwidth beside the spec
-            try:
-                roof["measured_read_peak"] = round(rnd.measure_read_bw(4 << 30), 1)
-            except Exception as e:  # reported, never fatal to the bench line
-                roof["measured_read_peak"] = "unavailable: %s" % e
+            roof["ref_traversal_equiv_GBps"] = round(b_seg * seg_per_launch / avg_launch_s / 1e9, 1)
+            roof["ref_traversal_B_seg"] = round(b_seg, 1)
+        # the measured streaming-read bandwidth beside the spec
+        try:
+            roof["measured_read_peak"] = round(rnd.measure_read_bw(4 << 30), 1)
+        except Exception as e:  # reported, never fatal to the bench line
+            roof["measured_read_peak"] = "unavailable: %s" % e
         cpu = None
         if n == 1 and not args.no_cpu and args.workload == "C2":
             cpu = cpu_baseline(data, cam, h_img)
         out = {"metric": METRIC, "value": round(value, 2), "unit": "Msamples/s", "n_gpus": n, "steps": args.steps,
                "warmup": args.warmup, "ms_per_step": round(elapsed * 1e3 / args.steps, 4),
-               "higher_is_better": True, "scaling": "strong" if strong else "weak", "vs_baseline": None,
+               "higher_is_better": True, "scaling": "strong", "vs_baseline": None,
                "dtype": "f32",
                "data": "synthetic seeds; " + ("Scene/cbox geometry recovered from the reference's cbox.mb"
                                               if args.workload == "C2" else "see config.workload"),
                "config": {"workload": wl["desc"],
-                          "width": W, "height_per_gpu": h_img // n if strong else H_PER_GPU, "max_depth": DEPTH,
+                          "width": W, "height": h_img, "max_depth": DEPTH,
                           "parallelism": "row-stripe tiles x%d" % n, "mode": "exact",
                           "schedule": "paired" if dsc.schedule == L.SCHED_PAIRED else "single",
                           "frames_per_block": fpb},
                "active_Msegments_per_s": round(segments * n / elapsed / 1e6, 2),
                "image_reduce_ms": None if reduce_ms is None else round(reduce_ms, 3),
+               "weak_scaling": weak,
                "roofline": roof, "cpu_baseline": cpu}
         print(json.dumps(out), flush=True)
     dsc.close()

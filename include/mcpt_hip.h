@@ -123,7 +123,7 @@ typedef struct mcpt_render_params {
   int32_t mode;                     /* MCPT_MODE_*                          */
   int32_t frames_per_launch;        /* frames per block (a lane runs one pixel
                                        for one block, then hands it on);
-                                       <= 0: auto, 4..16 by load balance */
+                                       <= 0: auto (mcpt_tuning.block_entries) */
   int32_t schedule;                 /* MCPT_SCHED_*: how k_render batches leaf
                                        tests (results identical; speed only) */
 } mcpt_render_params;
@@ -151,7 +151,34 @@ typedef struct mcpt_stats {
   uint64_t wave_shade_phases;
   uint64_t order_fallbacks;         /* EXACT: segments re-searched in the     */
                                     /*  reference's left-first order         */
+  uint64_t wave_iterations;         /* k_render loop iterations, all waves    */
+  uint64_t lane_waiting;            /* lane-iterations spent waiting for the
+                                       previous frame block of its pixel     */
+  uint64_t lane_idle;               /* lane-iterations with no pixel (queue
+                                       claim pending, or the launch's tail)  */
+  int32_t  stack_window;            /* 1: the last call ran the LDS-window stack */
+  int32_t  workgroups;              /* 64-lane workgroups per launch (resident grid) */
 } mcpt_stats;
+
+/* Launch-plan knobs of the fused kernel (speed only: every setting gives the
+ * same bits).  A zero-initialised struct means "defaults"; each field <= 0
+ * keeps its default.  Replaces the environment knobs of earlier builds:
+ * nothing is read from the environment on the render path. */
+typedef struct mcpt_tuning {
+  int32_t leaf_threshold;   /* lanes with a pending leaf before the L phase runs
+                               (default 4 single / 16 paired schedule)          */
+  int32_t shade_threshold;  /* lanes waiting before the S phase runs (32)        */
+  int32_t queue_chunk;      /* queue entries a wave claims per atomic (4)        */
+  int32_t block_entries;    /* auto frames-per-block: smallest block count that
+                               gives every resident lane this many queue entries
+                               (32)                                              */
+  int32_t max_block_frames; /* auto frames-per-block upper bound (32)            */
+  int32_t stack_window;     /* 0 auto (default), 1 the 32-entry LDS window with
+                               a global spill, 2 the whole stack in LDS          */
+  int32_t lds_pad;          /* extra LDS bytes per workgroup (occupancy
+                               experiments; 0)                                    */
+  int32_t queues;           /* work queues (1..8; 8: one per XCD)              */
+} mcpt_tuning;
 
 /* ------------------------------------------------------- version / errors */
 const char *mcpt_version(void);
@@ -222,10 +249,32 @@ int mcpt_scene_destroy(mcpt_scene *scene);
  * (intersect, shade) -> history accumulate, exactly the per-pixel effect of
  * OpenCL::update (OpenCLApp.cpp:57-82) + ColorOut (colorout.cpp:40-73).
  * seeds/hist/count are W*H device arrays (u32, float4, i32) that persist
- * across calls; pixels outside this GPU's stripes are left untouched.    */
+ * across calls; pixels outside this GPU's stripes are left untouched.
+ * Stream-ordered and asynchronous: the call enqueues its work on `stream`
+ * and returns (mcpt_get_stats waits for it).  One stream per context at a
+ * time: the context's queue heads and hand-off area are reused by every
+ * call.                                                                  */
 int mcpt_render_frames(mcpt_ctx *ctx, const mcpt_scene *scene, const mcpt_camera *cam,
                        const mcpt_render_params *params, uint32_t *seeds_dev,
                        float *hist_dev, int32_t *count_dev, void *stream);
+
+/* Launch-plan knobs (speed only), kept in the context; NULL resets them.  */
+int mcpt_set_tuning(mcpt_ctx *ctx, const mcpt_tuning *tuning);
+int mcpt_get_tuning(mcpt_ctx *ctx, mcpt_tuning *out);
+
+/* Per-image state in HBM for C/C++ hosts that do not manage device memory
+ * themselves: the reference's randBuffer (scenebuild.cpp:113-120),
+ * frameBuffer and sampleCount (colorout.cpp), W*H each.  create copies the
+ * host seeds in and zeroes mean and count; buffers() returns the device
+ * pointers mcpt_render_frames takes; download copies any of them back to
+ * host arrays (NULL skips one) after the context's work on `stream` is done
+ * (ColorOut's dump read, colorout.cpp:55-68).                            */
+typedef struct mcpt_state mcpt_state;
+int mcpt_state_create(mcpt_ctx *ctx, int32_t width, int32_t height, const uint32_t *seeds_host, mcpt_state **out);
+int mcpt_state_buffers(mcpt_state *st, uint32_t **seeds_dev, float **hist_dev, int32_t **count_dev);
+int mcpt_download(mcpt_ctx *ctx, const mcpt_state *st, float *hist_rgba, int32_t *count, uint32_t *seeds,
+                  void *stream);
+int mcpt_state_destroy(mcpt_state *st);
 
 /* Wavefront kernels on the reference's AoS records, one per reference
  * kernel, for drop-in use and kernel-level parity:                       */
@@ -243,7 +292,8 @@ int mcpt_shade(mcpt_ctx *ctx, const mcpt_scene *scene, mcpt_ray *rays_dev,
 int mcpt_accumulate(mcpt_ctx *ctx, float *color_dev, float *hist_dev, int32_t *count_dev,
                     int64_t n, int32_t max_attempt, void *stream);
 
-/* Counters of the last render call (segments etc. need stats enabled).   */
+/* Counters of the last render call (segments etc. need stats enabled);
+ * waits for that call's work to finish.                                   */
 int mcpt_set_stats(mcpt_ctx *ctx, int32_t enabled);
 int mcpt_get_stats(mcpt_ctx *ctx, mcpt_stats *out);
 
@@ -281,6 +331,15 @@ int mcpt_bvh_lcv_device(const mcpt_bvh_node *nodes_dev, int64_t n_nodes, const m
  * `bytes` after a warm-up): the measured roofline denominator SURVEY.md
  * §8(d) asks for next to the 8 TB/s spec.                                 */
 int mcpt_measure_read_bw(mcpt_ctx *ctx, int64_t bytes, double *gbps);
+
+/* Counter calibration for the roofline: gathers every
+ * record of a fresh table_bytes table (a power of two, evicted from the
+ * Infinity Cache first) once, in scrambled order, as whole record_bytes
+ * records (64: k_render's triangles, 128: its nodes) with one 16-B load per
+ * lane and slot.  The known byte count is table_bytes; rocprofv3's
+ * FETCH_SIZE for kernel k_gather_probe against it gives the counter's scale
+ * for this access shape.  *ms = the kernel's device time.                  */
+int mcpt_gather_probe(mcpt_ctx *ctx, int32_t record_bytes, int64_t table_bytes, double *ms);
 
 /* Device self-check of the inline sin/cos used by randomDirection
  * (shade.cl:40-59) against the ocml library calls the reference kernel

@@ -45,7 +45,16 @@ class Stats(ctypes.Structure):
                 ("tri_tests", ctypes.c_uint64), ("bad_material", ctypes.c_uint64),
                 ("kernel_ms", ctypes.c_double), ("launches", ctypes.c_int32), ("frames_per_block", ctypes.c_int32),
                 ("wave_node_phases", ctypes.c_uint64), ("wave_leaf_phases", ctypes.c_uint64),
-                ("wave_shade_phases", ctypes.c_uint64), ("order_fallbacks", ctypes.c_uint64)]
+                ("wave_shade_phases", ctypes.c_uint64), ("order_fallbacks", ctypes.c_uint64),
+                ("wave_iterations", ctypes.c_uint64), ("lane_waiting", ctypes.c_uint64), ("lane_idle", ctypes.c_uint64),
+                ("stack_window", ctypes.c_int32), ("workgroups", ctypes.c_int32)]
+
+
+class Tuning(ctypes.Structure):
+    """mcpt_tuning: launch-plan knobs of k_render (speed only; 0 = default)."""
+    _fields_ = [(n, ctypes.c_int32) for n in (
+        "leaf_threshold", "shade_threshold", "queue_chunk", "block_entries", "max_block_frames", "stack_window",
+        "lds_pad", "queues")]
 
 
 class MCPTError(RuntimeError):
@@ -81,10 +90,17 @@ SIGNATURES = {
     "mcpt_intersect": (_I32, [_P, _P, _P, _I64, _P, _F32, _I32, _P]),
     "mcpt_shade": (_I32, [_P, _P, _P, _P, _P, _P, _I64, _I32, _P]),
     "mcpt_accumulate": (_I32, [_P, _P, _P, _P, _I64, _I32, _P]),
+    "mcpt_set_tuning": (_I32, [_P, _P]),
+    "mcpt_get_tuning": (_I32, [_P, _P]),
+    "mcpt_state_create": (_I32, [_P, _I32, _I32, _P, _P]),
+    "mcpt_state_buffers": (_I32, [_P, _P, _P, _P]),
+    "mcpt_download": (_I32, [_P, _P, _P, _P, _P, _P]),
+    "mcpt_state_destroy": (_I32, [_P]),
     "mcpt_set_stats": (_I32, [_P, _I32]),
     "mcpt_get_stats": (_I32, [_P, _P]),
     "mcpt_selfcheck_trig": (_I32, [_P, _P, _P]),
     "mcpt_measure_read_bw": (_I32, [_P, _I64, _P]),
+    "mcpt_gather_probe": (_I32, [_P, _I32, _I64, _P]),
     "mcpt_build_hlbvh_device": (_I32, [_P, _I64, _P, _P]),
     "mcpt_treelet_device": (_I32, [_P, _I64, _P]),
     "mcpt_bvh_sah": (_I32, [_P, _I64, _P]),
@@ -112,6 +128,8 @@ def lib():
             pass
         so = ctypes.CDLL(LIB_PATH)
         for name, (res, args) in SIGNATURES.items():
+            if os.environ.get("MCPT_LIB_OVERRIDE") and not hasattr(so, name):
+                continue  # an older build under A/B timing (tools/ab.py) may lack newer entry points
             fn = getattr(so, name)
             fn.restype = res
             fn.argtypes = args

@@ -109,19 +109,42 @@ struct mcpt_scene {
   SceneView view;
 };
 
+constexpr int kQueues = 8;         // k_render work queues (at most): one per XCD (MI355X has 8)
+constexpr int kQueueStride = 32;   // u32 words between queue heads: one 128-B line each
+constexpr int kHandoffWords = 6;   // seed, mean.xyzw, count: one tagged 8-B granule each
+constexpr int kStatSlots = 16;     // k_render counters (mcpt_stats)
+
 struct mcpt_ctx {
   int device;
+  int n_cu = 0;
   bool stats_on = false;
   unsigned long long *d_stats = nullptr;  // segments, nodes, tris, bad, wave T/L/S phases
-  uint32_t *d_queue = nullptr;            // k_render work-queue heads, one per launch
-  int32_t queue_cap = 0;
-  int32_t *d_progress = nullptr;          // k_render per-pixel block progress
-  int64_t progress_cap = 0;
+  uint32_t *d_queue = nullptr;            // k_render work-queue heads, kQueues per launch
+  int32_t queue_cap = 0;                  // launches the head array holds
+  unsigned long long *d_handoff = nullptr;  // k_render per-pixel block hand-off granules
+  int64_t handoff_cap = 0;                // pixels
+  uint32_t launch_seq = 0;                // tags hand-off granules with the launch they belong to
   int32_t *d_spill = nullptr;             // k_render WindowStack spill areas
   int64_t spill_cap = 0;
-  int32_t resident_blocks[2] = {0, 0};   // occupancy of k_render<EXACT|NOPRUNE> (64-thread blocks/CU)
+  mcpt_tuning tune;                       // launch-plan knobs (mcpt_set_tuning)
+  struct Occ {
+    const void *fn;
+    size_t lds;
+    int per_cu;
+  };
+  std::vector<Occ> occ;                   // occupancy per (kernel, LDS bytes), queried once
   mcpt_stats last;
+  bool last_pending = false;              // the last render call's events/counters not read yet
+  bool last_stats = false;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
+};
+
+struct mcpt_state {
+  int device;
+  int32_t width, height;
+  uint32_t *seeds = nullptr;
+  float *hist = nullptr;
+  int32_t *count = nullptr;
 };
 
 #define HIP_OK(expr)                                                                        \
@@ -537,15 +560,26 @@ __device__ inline f4 accumulate_one(f4 now, f4 &hist, int32_t &cnt, int max_atte
 }
 
 // --------------------------------------------------------- fused hot kernel
-// Accesses that hand a pixel's state from one lane to another inside a launch.
-// They bypass the per-CU and per-XCD caches (sc0 sc1), so they meet in memory
-// whichever XCDs the two lanes run on.
-__device__ inline int32_t sys_load(const int32_t *p) {
-  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+// Block hand-off: a pixel's state passes from the lane that ran frame block
+// b-1 to the lane that runs block b as six 8-byte granules {tag:32 | word:32}
+// (seed, mean.xyzw, count), each written and read by ONE agent-scope atomic
+// (global_store/load_dwordx2 sc1: bypasses the CU's L1; coherent across the
+// XCDs' L2s).  The reader accepts a granule only when its tag names this
+// launch and block b, so every word it keeps is the one the writer stored
+// with that tag: per-location coherence of the atomics is all the protocol
+// needs, no flag and no fence orders anything (MI355X_MICROARCH.md,
+// "handoff-1to1": data-tagged granules are the cheapest hand-off).
+__device__ inline unsigned long long handoff_load(const unsigned long long *p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
-__device__ inline void sys_store(int32_t *p, int32_t v) {
-  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+__device__ inline void handoff_store(unsigned long long *p, unsigned long long v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
+// This wave's XCD (0-7).  Picks the home queue: speed only — any placement
+// gives the same result, and waves steal from the other queues when theirs
+// runs dry (MI355X_MICROARCH.md, "dequeue": one head word saturates at about
+// 88 dequeues/us; sharded per XCD the rate scales with the heads).
+__device__ inline uint32_t xcc_id() { return __builtin_amdgcn_s_getreg((3 << 11) | 20) & 7u; }  // hwreg(HW_REG_XCC_ID, 0, 4)
 
 struct RenderArgs {
   mcpt_camera cam;
@@ -558,10 +592,12 @@ struct RenderArgs {
   int32_t stripe_rows, stripe_index, stripe_count;
   int32_t max_depth, max_attempt, frame_begin, frames;  // frames: of this launch
   int32_t fpl, blocks;         // frames per block, blocks in this launch
-  int32_t *progress;           // per pixel: blocks published in this launch
+  unsigned long long *handoff; // per pixel: kHandoffWords tagged granules
+  uint32_t tag_base;           // this launch's tag; a granule for block b carries tag_base | b
   int32_t stack_depth;
   int32_t th_leaf, th_shade;  // lanes waiting before the L / S phase runs
-  uint32_t *queue;            // work-queue head (zeroed before each launch)
+  uint32_t *queue;            // n_queues work-queue heads, kQueueStride apart (zeroed before each launch)
+  uint32_t n_queues;          // 1..kQueues
   int32_t lds_mats;           // 1: copy the material table to LDS after the stack
   int32_t chunk;              // queue entries a wave claims per atomic (at least)
   int32_t *spill;             // WindowStack spill areas, one per resident lane
@@ -575,14 +611,22 @@ __device__ inline int32_t global_row(int32_t lr, const RenderArgs &A) {
 
 constexpr float kTmin = 0.001f;  // host EPSILON passed as tmin (oclbasic.h:193, scenebuild.cpp:125)
 
+// Queue x of nq holds the 8x8 tiles t with t % nq == x: queue_items pixel
+// slots, each entry q = block * items + slot (block-major).
+__device__ inline uint32_t queue_items(uint32_t x, uint32_t n_tiles, uint32_t nq) {
+  return x < n_tiles ? ((n_tiles - 1u - x) / nq + 1u) * 64u : 0u;
+}
+
 // The fused kernel is a persistent per-wave state machine.
 //
-// Work queue: a launch renders `frames` frames of every pixel of this GPU's
-// stripes.  Pixels are handed out in 8x8-tile order by one atomic counter;
-// a lane owns a pixel for all of its frames (the seed chain and the running
-// mean are sequential per pixel), writes the pixel back when done and pulls
-// the next one, so lanes whose paths were short keep working instead of
-// idling until the wave's slowest pixel finishes.
+// Work queues: a launch renders `frames` frames of every pixel of this GPU's
+// stripes, in frame blocks.  (pixel, block) entries are handed out in 8x8-tile
+// order from n_queues atomic counters, one per XCD (tiles dealt round-robin);
+// a wave takes from its own XCD's queue and steals from the others when that
+// one runs dry.  A lane owns a pixel for one block of frames (the seed chain
+// and the running mean are sequential per pixel), hands the state on when
+// done and pulls the next entry, so lanes whose paths were short keep working
+// instead of idling until the wave's slowest pixel finishes.
 //
 // Phases.  Every lane with a pixel is in one of
 //   T: walking internal BVH nodes (cur >= 0)
@@ -619,11 +663,15 @@ __global__ void __launch_bounds__(64, MCPT_WAVES_PER_SIMD) k_render(RenderArgs A
 
   unsigned long long n_seg = 0, n_nodes = 0, n_tests = 0, n_bad = 0;
   unsigned long long w_t = 0, w_l = 0, w_s = 0, n_fb = 0;
-  // pixel state
-  bool alive = true;   // queue not exhausted for this lane
-  bool has_px = false; // owns a pixel
-  int32_t pid = 0, f = 0, cnt = 0;
-  uint32_t seed = 0, pxy = 0;  // pxy = x | y << 16
+  unsigned long long w_it = 0, n_wait = 0, n_idle = 0;
+  // pixel state.  lst: this lane's role in the queue protocol, one small
+  // int (one VGPR; kept out of lane-mask SGPR pairs on purpose, SGPRs are
+  // the scarce register file of this kernel)
+  constexpr int32_t kBusy = 0, kNeed = 1, kPend = 2, kDead = 3;
+  int32_t lst = kNeed;
+  int32_t f = 0, cnt = 0;
+  uint32_t seed = 0, pxy = 0;  // pxy = x | y << 16 (the pending entry's pixel while kPend)
+  int32_t blk = 0;             // frame block of the pixel (the pending entry's block while kPend)
   f4 hist = (f4){0.0f, 0.0f, 0.0f, 0.0f};
   f4 o = hist, d = hist, color = hist;
   // uniform generateRay constants, moved to scalar registers
@@ -656,85 +704,116 @@ __global__ void __launch_bounds__(64, MCPT_WAVES_PER_SIMD) k_render(RenderArgs A
     else
       cur = kDone;
   };
-  // queue entry q = block * n_items + item: frame block q / n_items of pixel
-  // slot q % n_items (8x8 tiles).  Blocks of one pixel run in order: the
-  // lane that takes (p, b > 0) waits until the lane that ran (p, b - 1)
-  // has published its state (A.progress[p] = b).
-  const uint32_t n_items = (uint32_t)A.tiles_x * (uint32_t)((A.local_rows + 7) >> 3) * 64u;
-  const uint32_t n_total = n_items * (uint32_t)A.blocks;
-  uint32_t pool = 0, pool_left = 0;  // wave-uniform: claimed, not yet started queue entries
-  bool pending = false;              // holds entry pq, not started yet
-  uint32_t pq = 0;
-  int32_t blk = 0;
+  // Queue entry q of queue x = block * items + slot: frame block q / items of
+  // pixel slot q % items of that queue's tiles.  Blocks of one pixel run in
+  // order: the lane that takes (p, b > 0) waits until the lane that ran
+  // (p, b - 1) has published its granules with tag (tag_base | b).
+  // No deadlock: every entry waits only for an entry of the same queue with
+  // a lower index, entries are claimed in index order, and a wave starts all
+  // its claimed entries before it claims more.
+  const uint32_t n_tiles = (uint32_t)A.tiles_x * (uint32_t)((A.local_rows + 7) >> 3);
+  const uint32_t nq = A.n_queues;
+  // wave-uniform queue state, packed into one SGPR: bits 0-3 the queue claims
+  // go to, 4-7 the queue of the pool, 8-11 queues found dry, bit 12 "the
+  // claim queue ran dry: the next claim moves on"
+  uint32_t qs = (xcc_id() % nq) * 0x11u;
+  uint32_t pool = 0, pool_left = 0;  // wave-uniform: claimed, unassigned entries of queue (qs >> 4) & 15
 
   for (;;) {
     // ---- fetch: lanes without work take the next queue entries, from the
     // wave's pool of claimed entries; one atomic claims max(chunk, shortfall)
     {
-      const bool need = alive && !has_px && !pending;
-      const unsigned long long mn = __ballot(need);
+      const unsigned long long mn = __ballot(lst == kNeed);
       if (mn) {
         const uint32_t n_need = (uint32_t)__popcll(mn);
         const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(mn >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mn, 0));
-        uint32_t q = pool + rank;
+        uint32_t q = pool + rank, qx = (qs >> 4) & 15u;
+        bool got = rank < pool_left;
         if (n_need <= pool_left) {
           pool += n_need;
           pool_left -= n_need;
         } else {
-          const uint32_t claim = max((uint32_t)A.chunk, n_need - pool_left);
-          const int leader = __builtin_ctzll(mn);
-          uint32_t base = 0;
-          if (lane == leader) base = atomicAdd(A.queue, claim);
-          base = __builtin_amdgcn_readfirstlane(__shfl(base, leader));
-          if (rank >= pool_left) q = base + (rank - pool_left);
-          pool = base + (n_need - pool_left);
-          pool_left = claim - (n_need - pool_left);
-        }
-        if (need) {
-          if (q >= n_total) {
-            alive = false;
+          if (qs & 0x1000u) {  // steal: the next queue round the ring
+            const uint32_t nxt = (qs & 15u) + 1u == nq ? 0u : (qs & 15u) + 1u;
+            qs = (qs & 0x0F0u) + 0x100u * (((qs >> 8) & 15u) + 1u) + nxt;
+          }
+          const uint32_t qid = qs & 15u;
+          const uint32_t shortfall = n_need - pool_left;
+          if (((qs >> 8) & 15u) < nq) {
+            const uint32_t claim = max((uint32_t)A.chunk, shortfall);
+            const uint32_t total = queue_items(qid, n_tiles, nq) * (uint32_t)A.blocks;
+            const int leader = __builtin_ctzll(mn);
+            uint32_t base = 0;
+            if (lane == leader) base = atomicAdd(A.queue + qid * kQueueStride, claim);
+            base = __builtin_amdgcn_readfirstlane(__shfl(base, leader));
+            if (!got) {
+              q = base + (rank - pool_left);
+              qx = qid;
+              got = q < total;
+            }
+            pool = base + shortfall;
+            pool_left = claim - shortfall;
+            qs = (qs & ~0xF0u) | (qid << 4);
+            if (base + claim >= total) {  // the queue is dry after this claim
+              qs |= 0x1000u;
+              pool_left = pool < total ? min(pool_left, total - pool) : 0u;
+            }
           } else {
-            pending = true;
-            pq = q;
+            pool_left = 0;
+          }
+        }
+        if (lst == kNeed) {
+          if (got) {
+            const uint32_t items = queue_items(qx, n_tiles, nq);
+            const uint32_t b = q / items, j = q - b * items;
+            const int32_t tile = (int32_t)((j >> 6) * nq + qx), k = (int32_t)(j & 63u);
+            const int32_t x = (tile % A.tiles_x) * 8 + (k & 7);
+            const int32_t lr = (tile / A.tiles_x) * 8 + (k >> 3);
+            const int32_t y = lr < A.local_rows ? global_row(lr, A) : A.H;
+            if (x < A.W && y < A.H) {  // else an edge-tile hole: fetch again
+              lst = kPend;
+              blk = (int32_t)b;
+              pxy = (uint32_t)x | ((uint32_t)y << 16);
+            }
+          } else if (((qs >> 8) & 15u) >= nq) {
+            lst = kDead;  // every queue is dry
           }
         }
       }
-      if (pending) {  // start the entry once its pixel's previous block is published
-        const uint32_t b = pq / n_items, it = pq - b * n_items;
-        const int32_t tile = (int32_t)(it >> 6), k = (int32_t)(it & 63);
-        const int32_t x = (tile % A.tiles_x) * 8 + (k & 7);
-        const int32_t lr = (tile / A.tiles_x) * 8 + (k >> 3);
-        const int32_t y = lr < A.local_rows ? global_row(lr, A) : A.H;
-        if (x >= A.W || y >= A.H) {  // an edge-tile hole: fetch again
-          pending = false;
-        } else {
-          const int32_t p = y * A.W + x;
-          if (b == 0) {  // state from before this launch
-            pending = false;
-            seed = A.seeds[p];
-            hist = A.hist[p];
-            cnt = A.count[p];
-          } else if (sys_load(&A.progress[p]) >= (int32_t)b) {  // published by another lane, any XCD
-            pending = false;
-            seed = (uint32_t)sys_load((const int32_t *)&A.seeds[p]);
-            const int32_t *hp = (const int32_t *)&A.hist[p];
-            hist = (f4){as_f(sys_load(hp)), as_f(sys_load(hp + 1)), as_f(sys_load(hp + 2)), as_f(sys_load(hp + 3))};
-            cnt = sys_load(&A.count[p]);
-          }
-          if (!pending) {
-            has_px = true;
-            blk = (int32_t)b;
-            pid = p;
-            f = 0;
-            pxy = (uint32_t)x | ((uint32_t)y << 16);
-            primary();
-            begin_segment();
-          }
+      if (lst == kPend) {  // start the entry once its pixel's previous block is published
+        const int32_t pp = (int32_t)(pxy >> 16) * A.W + (int32_t)(pxy & 0xFFFFu);
+        bool ready = true;
+        if (blk == 0) {  // state from before this launch
+          seed = A.seeds[pp];
+          hist = A.hist[pp];
+          cnt = A.count[pp];
+        } else {  // published by another lane, any XCD
+          const unsigned long long *g = A.handoff + (size_t)pp * kHandoffWords;
+          const unsigned long long g0 = handoff_load(g), g1 = handoff_load(g + 1), g2 = handoff_load(g + 2);
+          const unsigned long long g3 = handoff_load(g + 3), g4 = handoff_load(g + 4), g5 = handoff_load(g + 5);
+          const uint32_t want = A.tag_base | (uint32_t)blk;
+          ready = (uint32_t)(g0 >> 32) == want && (uint32_t)(g1 >> 32) == want && (uint32_t)(g2 >> 32) == want &&
+                  (uint32_t)(g3 >> 32) == want && (uint32_t)(g4 >> 32) == want && (uint32_t)(g5 >> 32) == want;
+          seed = (uint32_t)g0;
+          hist = (f4){as_f((int32_t)(uint32_t)g1), as_f((int32_t)(uint32_t)g2), as_f((int32_t)(uint32_t)g3),
+                      as_f((int32_t)(uint32_t)g4)};
+          cnt = (int32_t)(uint32_t)g5;
+        }
+        if (ready) {
+          lst = kBusy;
+          f = 0;
+          primary();
+          begin_segment();
         }
       }
     }
-    if (!__ballot(alive)) break;
-    const bool live = has_px;
+    if (!__ballot(lst != kDead)) break;
+    const bool live = lst == kBusy;
+    if (STATS) {
+      if (lane == __builtin_ctzll(__ballot(1))) w_it++;
+      n_wait += lst == kPend;
+      n_idle += lst == kNeed || lst == kDead;  // no claim yet, an edge hole, or out of work (tail)
+    }
     // ---- T: one node step (objdef.h:252-273 with child boxes)
     const bool in_t = live && cur >= 0;
     if (__ballot(in_t)) {
@@ -839,25 +918,25 @@ __global__ void __launch_bounds__(64, MCPT_WAVES_PER_SIMD) k_render(RenderArgs A
           const int32_t fend = min(A.fpl, A.frames - f0);
           if (f < fend) primary();
           if (f == fend) {  // block complete: write back, fetch another next iteration
+            const int32_t pid = (int32_t)(pxy >> 16) * A.W + (int32_t)(pxy & 0xFFFFu);
             if (blk + 1 < A.blocks) {  // publish for the lane that takes the next block
-              sys_store((int32_t *)&A.seeds[pid], (int32_t)seed);
-              int32_t *hp = (int32_t *)&A.hist[pid];
-              sys_store(hp, as_i(hist.x));
-              sys_store(hp + 1, as_i(hist.y));
-              sys_store(hp + 2, as_i(hist.z));
-              sys_store(hp + 3, as_i(hist.w));
-              sys_store(&A.count[pid], cnt);
-              asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // state reaches memory before the flag
-              sys_store(&A.progress[pid], blk + 1);
+              const unsigned long long tag = (unsigned long long)(A.tag_base | (uint32_t)(blk + 1)) << 32;
+              unsigned long long *g = A.handoff + (size_t)pid * kHandoffWords;
+              handoff_store(g, tag | seed);
+              handoff_store(g + 1, tag | (uint32_t)as_i(hist.x));
+              handoff_store(g + 2, tag | (uint32_t)as_i(hist.y));
+              handoff_store(g + 3, tag | (uint32_t)as_i(hist.z));
+              handoff_store(g + 4, tag | (uint32_t)as_i(hist.w));
+              handoff_store(g + 5, tag | (uint32_t)cnt);
             } else {
               A.seeds[pid] = seed;
               A.hist[pid] = hist;
               A.count[pid] = cnt;
             }
-            has_px = false;
+            lst = kNeed;
           }
         }
-        if (has_px) begin_segment();
+        if (lst == kBusy) begin_segment();
       }
     }
   }
@@ -872,6 +951,9 @@ __global__ void __launch_bounds__(64, MCPT_WAVES_PER_SIMD) k_render(RenderArgs A
       atomicAdd(&A.stats[5], w_l);
       atomicAdd(&A.stats[6], w_s);
     }
+    if (w_it) atomicAdd(&A.stats[8], w_it);
+    if (n_wait) atomicAdd(&A.stats[9], n_wait);
+    if (n_idle) atomicAdd(&A.stats[10], n_idle);
   }
 }
 
@@ -983,7 +1065,9 @@ int mcpt_ctx_create(int32_t device, mcpt_ctx **out) {
   mcpt_ctx *c = new mcpt_ctx();
   c->device = device;
   std::memset(&c->last, 0, sizeof(c->last));
-  if (hipMalloc(&c->d_stats, 8 * sizeof(unsigned long long)) != hipSuccess ||
+  std::memset(&c->tune, 0, sizeof(c->tune));
+  if (hipDeviceGetAttribute(&c->n_cu, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess ||
+      hipMalloc(&c->d_stats, kStatSlots * sizeof(unsigned long long)) != hipSuccess ||
       hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess) {
     delete c;
     return mcpt::fail(MCPT_ERR_HIP, "ctx_create: allocation failed");
@@ -996,8 +1080,9 @@ int mcpt_ctx_destroy(mcpt_ctx *c) {
   if (!c) return MCPT_OK;
   (void)hipSetDevice(c->device);
   if (c->d_stats) (void)hipFree(c->d_stats);
+  if (c->last_pending && c->ev1) (void)hipEventSynchronize(c->ev1);  // the last render may still use the buffers
   if (c->d_queue) (void)hipFree(c->d_queue);
-  if (c->d_progress) (void)hipFree(c->d_progress);
+  if (c->d_handoff) (void)hipFree(c->d_handoff);
   if (c->d_spill) (void)hipFree(c->d_spill);
   if (c->ev0) (void)hipEventDestroy(c->ev0);
   if (c->ev1) (void)hipEventDestroy(c->ev1);
@@ -1075,6 +1160,61 @@ int mcpt_measure_read_bw(mcpt_ctx *c, int64_t bytes, double *gbps) {
   return MCPT_OK;
 }
 
+// Calibration of the memory-side byte counters (rocprofv3 FETCH_SIZE) for
+// k_render's access shape: each lane gathers whole records of 4 or 8 float4
+// (64-B triangles, 128-B nodes) with one dwordx4 load per 16 B, at scrambled
+// record indices, every record of the table exactly once
+// (mcpt_gather_probe).
+__global__ void __launch_bounds__(256) k_gather_probe(const f4 *__restrict__ tab, uint64_t n_rec, int words,
+                                                      float *sink) {
+  f4 acc = (f4){0.0f, 0.0f, 0.0f, 0.0f};
+  const uint64_t stride = (uint64_t)gridDim.x * 256;
+  for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n_rec; i += stride) {
+    const uint64_t r = (i * 0x9E3779B97F4A7C15ull) & (n_rec - 1);  // odd multiplier: a bijection mod 2^k
+    const f4 *p = tab + r * (uint64_t)words;
+    if (words == 8) {
+      acc += p[0] + p[1] + p[2] + p[3] + p[4] + p[5] + p[6] + p[7];
+    } else {
+      acc += p[0] + p[1] + p[2] + p[3];
+    }
+  }
+  const float v = acc.x + acc.y + acc.z + acc.w;
+  if (v == 12345.678f) sink[blockIdx.x] = v;  // never true for the zeroed table
+}
+
+int mcpt_gather_probe(mcpt_ctx *c, int32_t record_bytes, int64_t table_bytes, double *ms_out) {
+  if (!c || !ms_out || (record_bytes != 64 && record_bytes != 128) || table_bytes < (1 << 20) ||
+      (table_bytes & (table_bytes - 1)) != 0)
+    return mcpt::fail(MCPT_ERR_ARG, "gather_probe: record 64/128 B, table a power of two >= 1 MiB");
+  HIP_OK(hipSetDevice(c->device));
+  void *tab = nullptr, *flush = nullptr;
+  float *sink = nullptr;
+  const size_t flush_bytes = (size_t)1 << 30;  // evicts the table from the 256 MiB Infinity Cache after the fill
+  if (hipMalloc(&tab, (size_t)table_bytes) != hipSuccess || hipMalloc(&flush, flush_bytes) != hipSuccess ||
+      hipMalloc(&sink, (size_t)c->n_cu * 32 * sizeof(float)) != hipSuccess ||
+      hipMemset(tab, 0, (size_t)table_bytes) != hipSuccess || hipMemset(flush, 1, flush_bytes) != hipSuccess ||
+      hipDeviceSynchronize() != hipSuccess) {
+    if (tab) (void)hipFree(tab);
+    if (flush) (void)hipFree(flush);
+    if (sink) (void)hipFree(sink);
+    return mcpt::fail(MCPT_ERR_HIP, "gather_probe: setup");
+  }
+  const uint64_t n_rec = (uint64_t)table_bytes / (uint64_t)record_bytes;
+  (void)hipEventRecord(c->ev0, 0);
+  hipLaunchKernelGGL(k_gather_probe, dim3(std::max(1, c->n_cu) * 32), dim3(256), 0, 0, (const f4 *)tab, n_rec,
+                     record_bytes / 16, sink);
+  (void)hipEventRecord(c->ev1, 0);
+  (void)hipEventSynchronize(c->ev1);
+  float ms = 0.0f;
+  (void)hipEventElapsedTime(&ms, c->ev0, c->ev1);
+  (void)hipFree(tab);
+  (void)hipFree(flush);
+  (void)hipFree(sink);
+  HIP_OK(hipGetLastError());
+  *ms_out = ms;
+  return MCPT_OK;
+}
+
 int mcpt_set_stats(mcpt_ctx *c, int32_t on) {
   if (!c) return mcpt::fail(MCPT_ERR_ARG, "set_stats: null ctx");
   c->stats_on = on != 0;
@@ -1083,7 +1223,98 @@ int mcpt_set_stats(mcpt_ctx *c, int32_t on) {
 
 int mcpt_get_stats(mcpt_ctx *c, mcpt_stats *out) {
   if (!c || !out) return mcpt::fail(MCPT_ERR_ARG, "get_stats: null");
+  if (c->last_pending) {  // the last render call was enqueued asynchronously: wait for it, then read
+    HIP_OK(hipSetDevice(c->device));
+    c->last_pending = false;
+    HIP_OK(hipEventSynchronize(c->ev1));
+    float ms = 0.0f;
+    HIP_OK(hipEventElapsedTime(&ms, c->ev0, c->ev1));
+    c->last.kernel_ms = ms;
+    if (c->last_stats) {
+      unsigned long long h[kStatSlots];
+      HIP_OK(hipMemcpy(h, c->d_stats, sizeof(h), hipMemcpyDeviceToHost));
+      c->last.segments = h[0];
+      c->last.node_visits = h[1];
+      c->last.tri_tests = h[2];
+      c->last.bad_material = h[3];
+      c->last.wave_node_phases = h[4];
+      c->last.wave_leaf_phases = h[5];
+      c->last.wave_shade_phases = h[6];
+      c->last.order_fallbacks = h[7];
+      c->last.wave_iterations = h[8];
+      c->last.lane_waiting = h[9];
+      c->last.lane_idle = h[10];
+    }
+  }
   *out = c->last;
+  return MCPT_OK;
+}
+
+int mcpt_set_tuning(mcpt_ctx *c, const mcpt_tuning *t) {
+  if (!c) return mcpt::fail(MCPT_ERR_ARG, "set_tuning: null ctx");
+  if (t && (t->stack_window < 0 || t->stack_window > 2 || t->lds_pad < 0 || t->lds_pad > 65536 ||
+            t->queue_chunk > 4096 || t->leaf_threshold > 64 || t->shade_threshold > 64))
+    return mcpt::fail(MCPT_ERR_ARG, "set_tuning: value out of range");
+  if (t)
+    c->tune = *t;
+  else
+    std::memset(&c->tune, 0, sizeof(c->tune));
+  return MCPT_OK;
+}
+
+int mcpt_get_tuning(mcpt_ctx *c, mcpt_tuning *out) {
+  if (!c || !out) return mcpt::fail(MCPT_ERR_ARG, "get_tuning: null");
+  *out = c->tune;
+  return MCPT_OK;
+}
+
+int mcpt_state_create(mcpt_ctx *c, int32_t w, int32_t h, const uint32_t *seeds, mcpt_state **out) {
+  if (!c || !seeds || !out || w <= 0 || h <= 0 || (int64_t)w * h > (int64_t)INT32_MAX)
+    return mcpt::fail(MCPT_ERR_ARG, "state_create: bad argument");
+  HIP_OK(hipSetDevice(c->device));
+  const size_t n = (size_t)w * h;
+  mcpt_state *s = new mcpt_state();
+  s->device = c->device;
+  s->width = w;
+  s->height = h;
+  if (hipMalloc(&s->seeds, n * 4) != hipSuccess || hipMalloc(&s->hist, n * 16) != hipSuccess ||
+      hipMalloc(&s->count, n * 4) != hipSuccess || hipMemcpy(s->seeds, seeds, n * 4, hipMemcpyHostToDevice) != hipSuccess ||
+      hipMemset(s->hist, 0, n * 16) != hipSuccess || hipMemset(s->count, 0, n * 4) != hipSuccess) {
+    mcpt_state_destroy(s);
+    return mcpt::fail(MCPT_ERR_HIP, "state_create: allocation or copy failed");
+  }
+  *out = s;
+  return MCPT_OK;
+}
+
+int mcpt_state_buffers(mcpt_state *s, uint32_t **seeds, float **hist, int32_t **count) {
+  if (!s) return mcpt::fail(MCPT_ERR_ARG, "state_buffers: null state");
+  if (seeds) *seeds = s->seeds;
+  if (hist) *hist = s->hist;
+  if (count) *count = s->count;
+  return MCPT_OK;
+}
+
+int mcpt_download(mcpt_ctx *c, const mcpt_state *s, float *hist, int32_t *count, uint32_t *seeds, void *stream) {
+  if (!c || !s || s->device != c->device) return mcpt::fail(MCPT_ERR_ARG, "download: bad argument");
+  HIP_OK(hipSetDevice(c->device));
+  hipStream_t st = (hipStream_t)stream;
+  const size_t n = (size_t)s->width * s->height;
+  if (hist) HIP_OK(hipMemcpyAsync(hist, s->hist, n * 16, hipMemcpyDeviceToHost, st));
+  if (count) HIP_OK(hipMemcpyAsync(count, s->count, n * 4, hipMemcpyDeviceToHost, st));
+  if (seeds) HIP_OK(hipMemcpyAsync(seeds, s->seeds, n * 4, hipMemcpyDeviceToHost, st));
+  HIP_OK(hipStreamSynchronize(st));
+  return MCPT_OK;
+}
+
+int mcpt_state_destroy(mcpt_state *s) {
+  if (!s) return MCPT_OK;
+  (void)hipSetDevice(s->device);
+  (void)hipDeviceSynchronize();  // work enqueued on the state may still be running
+  if (s->seeds) (void)hipFree(s->seeds);
+  if (s->hist) (void)hipFree(s->hist);
+  if (s->count) (void)hipFree(s->count);
+  delete s;
   return MCPT_OK;
 }
 
@@ -1281,6 +1512,21 @@ int mcpt_scene_destroy(mcpt_scene *s) {
   return MCPT_OK;
 }
 
+// Resident 64-lane workgroups per CU of a k_render instantiation at an LDS
+// size, asked once per (kernel, size) and kept in the context.
+static int occupancy(mcpt_ctx *ctx, const void *fn, size_t lds, int *out) {
+  for (const auto &e : ctx->occ)
+    if (e.fn == fn && e.lds == lds) {
+      *out = e.per_cu;
+      return MCPT_OK;
+    }
+  int n = 0;
+  HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, fn, 64, lds));
+  ctx->occ.push_back({fn, lds, n});
+  *out = n;
+  return MCPT_OK;
+}
+
 static int check_render(const mcpt_render_params *p) {
   if (p->width <= 0 || p->height <= 0 || p->max_depth <= 0 || p->max_depth > 0xFFFF || p->frames < 0 ||
       p->frame_begin < 0 || p->stripe_count <= 0 || p->stripe_rows <= 0 || p->stripe_index < 0 ||
@@ -1323,15 +1569,12 @@ int mcpt_render_frames(mcpt_ctx *ctx, const mcpt_scene *scene, const mcpt_camera
   A.stack_depth = scene->stack_depth;
   // tuned (tools/sweep_env.sh, tools/gpu_thr.sh): leaf phase at >= 4 lanes
   // (single-leaf schedule) or >= 16 (paired), shade at >= 32
+  const mcpt_tuning &T = ctx->tune;
   const bool pair = p->schedule == MCPT_SCHED_PAIRED;
-  A.th_leaf = pair ? 16 : 4;
-  A.th_shade = 32;
-  if (const char *e = std::getenv("MCPT_PHASE_THRESHOLDS")) {  // tuning knob: "leaf,shade"
-    int a = 0, b = 0;
-    if (std::sscanf(e, "%d,%d", &a, &b) == 2 && a >= 1 && b >= 1) A.th_leaf = a, A.th_shade = b;
-  }
-  A.chunk = 4;  // one queue atomic per >= 4 entries: the single counter's atomic rate binds below that
-  if (const char *e = std::getenv("MCPT_QUEUE_CHUNK")) A.chunk = std::max(1, std::min(4096, std::atoi(e)));  // tuning knob
+  A.th_leaf = T.leaf_threshold > 0 ? T.leaf_threshold : (pair ? 16 : 4);
+  A.th_shade = T.shade_threshold > 0 ? T.shade_threshold : 32;
+  A.chunk = T.queue_chunk > 0 ? T.queue_chunk : 4;  // queue entries per atomic (at least)
+  A.n_queues = T.queues > 0 ? (uint32_t)std::min(T.queues, kQueues) : (uint32_t)kQueues;
   const int64_t tiles = (int64_t)A.tiles_x * ((A.local_rows + 7) / 8);
   const int depth_entries = p->mode == MCPT_MODE_NOPRUNE ? scene->stack_depth : scene->stack_depth4;
   A.lds_mats = scene->n_mats <= 256 ? 1 : 0;
@@ -1342,31 +1585,34 @@ int mcpt_render_frames(mcpt_ctx *ctx, const mcpt_scene *scene, const mcpt_camera
   const bool noprune = p->mode == MCPT_MODE_NOPRUNE;
   // [noprune][stats][window][pair]
 #define MCPT_KR(M, ST, W) {(const void *)k_render<M, ST, W, false>, (const void *)k_render<M, ST, W, true>}
-  const void *kfns[2][2][2][2] = {
+  static const void *const kfns[2][2][2][2] = {
       {{MCPT_KR(MCPT_MODE_EXACT, false, false), MCPT_KR(MCPT_MODE_EXACT, false, true)},
        {MCPT_KR(MCPT_MODE_EXACT, true, false), MCPT_KR(MCPT_MODE_EXACT, true, true)}},
       {{MCPT_KR(MCPT_MODE_NOPRUNE, false, false), MCPT_KR(MCPT_MODE_NOPRUNE, false, true)},
        {MCPT_KR(MCPT_MODE_NOPRUNE, true, false), MCPT_KR(MCPT_MODE_NOPRUNE, true, true)}}};
 #undef MCPT_KR
-  const size_t lds_plain = (size_t)depth_entries * 64 * sizeof(int32_t) + lds_mats;
-  const size_t lds_win = (size_t)kStackWindow * 64 * sizeof(int32_t) + lds_mats;
-  int per_cu_plain = 0, per_cu_win = 0, n_cu = 0;
-  HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu_plain, kfns[noprune][ctx->stats_on][0][pair], 64, lds_plain));
-  HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu_win, kfns[noprune][ctx->stats_on][1][pair], 64, lds_win));
-  bool win = depth_entries > kStackWindow && per_cu_win > per_cu_plain;
-  if (const char *e = std::getenv("MCPT_STACK_WINDOW")) win = depth_entries > kStackWindow && std::atoi(e) != 0;  // tuning knob
-  const int per_cu_any = win ? per_cu_win : per_cu_plain;
-  size_t lds = win ? lds_win : lds_plain;
-  int per_cu = per_cu_any;
-  if (const char *e = std::getenv("MCPT_LDS_PAD")) {  // tuning knob: occupancy experiments (extra LDS per workgroup)
-    lds += (size_t)std::max(0, std::atoi(e));
-    HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kfns[noprune][ctx->stats_on][win][pair], 64, lds));
+  const size_t pad = (size_t)std::max(0, T.lds_pad);
+  const size_t lds_plain = (size_t)depth_entries * 64 * sizeof(int32_t) + lds_mats + pad;
+  const size_t lds_win = (size_t)kStackWindow * 64 * sizeof(int32_t) + lds_mats + pad;
+  bool win = false;
+  int per_cu = 0;
+  if (depth_entries > kStackWindow && T.stack_window != 2) {
+    int per_cu_plain = 0, per_cu_win = 0;
+    rc = occupancy(ctx, kfns[noprune][ctx->stats_on][0][pair], lds_plain, &per_cu_plain);
+    if (rc) return rc;
+    rc = occupancy(ctx, kfns[noprune][ctx->stats_on][1][pair], lds_win, &per_cu_win);
+    if (rc) return rc;
+    win = T.stack_window == 1 || per_cu_win > per_cu_plain;
+    per_cu = win ? per_cu_win : per_cu_plain;
+  } else {
+    rc = occupancy(ctx, kfns[noprune][ctx->stats_on][0][pair], lds_plain, &per_cu);
+    if (rc) return rc;
   }
+  const size_t lds = win ? lds_win : lds_plain;
   const void *kfn = kfns[noprune][ctx->stats_on][win][pair];
   A.stack_depth = win ? kStackWindow : depth_entries;  // the material table follows the stack in LDS
   A.spill_stride = win ? depth_entries - kStackWindow : 0;
-  HIP_OK(hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, ctx->device));
-  const int64_t grid = std::max<int64_t>(1, std::min<int64_t>(tiles, (int64_t)std::max(per_cu, 1) * n_cu));
+  const int64_t grid = std::max<int64_t>(1, std::min<int64_t>(tiles, (int64_t)std::max(per_cu, 1) * ctx->n_cu));
   const int64_t spill_need = win ? grid * 64 * (int64_t)A.spill_stride : 0;
   if (win && spill_need > ctx->spill_cap) {
     if (ctx->d_spill) HIP_OK(hipFree(ctx->d_spill));
@@ -1379,74 +1625,81 @@ int mcpt_render_frames(mcpt_ctx *ctx, const mcpt_scene *scene, const mcpt_camera
   // of frames, then hands the pixel's state to whichever lane takes its next
   // block.  One launch runs many blocks of every pixel, block-major, so lanes
   // stay busy until the last block (no per-block drain of the GPU).
-  // frames_per_launch <= 0: auto — blocks of 16 frames unless that leaves
-  // fewer than 16 queue entries per resident lane (short calls, strong-scaled
-  // ranks: load balance), then 8 or 4.  Smaller blocks on big calls lost on
-  // scenes with short paths (C3: 33.8 vs 56.3 G samples/s at 8 frames).
+  // frames_per_launch <= 0: auto — the fewest blocks that give every
+  // resident lane `block_entries` queue entries (so the launch's tail, where
+  // lanes run dry, is at most about 1/block_entries of it), frames split
+  // evenly over them, at most max_block_frames per block.
   const uint32_t n_items = (uint32_t)A.tiles_x * (uint32_t)((A.local_rows + 7) / 8) * 64u;
   int fpl = p->frames_per_launch;
   if (fpl <= 0) {
-    const double per_lane = (double)n_items * std::max(p->frames, 1) / (double)(grid * 64);
-    fpl = 16;
-    while (fpl > 4 && per_lane / fpl < 16.0) fpl /= 2;
+    const int frames = std::max(p->frames, 1);
+    const double per_block = (double)n_items / (double)(grid * 64);  // entries per lane per block
+    const int want = T.block_entries > 0 ? T.block_entries : 32;
+    const int cap = T.max_block_frames > 0 ? T.max_block_frames : 32;
+    int nb = (int)std::ceil(want / std::max(per_block, 1e-9));
+    nb = std::max(1, std::min(nb, frames));
+    fpl = (frames + nb - 1) / nb;
+    fpl = std::max(1, std::min(fpl, cap));
   }
-  const int64_t max_blocks = std::max<int64_t>(1, std::min<int64_t>(INT32_MAX / std::max<uint32_t>(n_items, 1), 4096 / fpl + 1));
+  // blocks per launch: the hand-off tag holds 12 bits of block index, and
+  // one launch covers at most ~4096 frames
+  const int64_t max_blocks = std::max<int64_t>(
+      1, std::min<int64_t>({(int64_t)INT32_MAX / std::max<uint32_t>(n_items, 1), 4096 / fpl + 1, 4095}));
   const int64_t n_blocks_all = (p->frames + fpl - 1) / fpl;
   const int n_launch = (int)((n_blocks_all + max_blocks - 1) / max_blocks);
-  if (n_launch > ctx->queue_cap) {  // one queue head per launch, zeroed by a single memset
+  if (n_launch > ctx->queue_cap) {  // kQueues heads per launch, zeroed by a single memset
     if (ctx->d_queue) HIP_OK(hipFree(ctx->d_queue));
     ctx->d_queue = nullptr;
     ctx->queue_cap = 0;
-    HIP_OK(hipMalloc(&ctx->d_queue, (size_t)std::max(n_launch, 64) * sizeof(uint32_t)));
-    ctx->queue_cap = std::max(n_launch, 64);
+    const int cap = std::max(n_launch, 64);
+    HIP_OK(hipMalloc(&ctx->d_queue, (size_t)cap * kQueues * kQueueStride * sizeof(uint32_t)));
+    ctx->queue_cap = cap;
   }
   const int64_t n_px = (int64_t)p->width * p->height;
-  if (n_blocks_all > 1 && n_px > ctx->progress_cap) {
-    if (ctx->d_progress) HIP_OK(hipFree(ctx->d_progress));
-    ctx->d_progress = nullptr;
-    ctx->progress_cap = 0;
-    HIP_OK(hipMalloc(&ctx->d_progress, (size_t)n_px * sizeof(int32_t)));
-    ctx->progress_cap = n_px;
+  if (n_blocks_all > 1 && n_px > ctx->handoff_cap) {
+    if (ctx->d_handoff) HIP_OK(hipFree(ctx->d_handoff));
+    ctx->d_handoff = nullptr;
+    ctx->handoff_cap = 0;
+    const size_t bytes = (size_t)n_px * kHandoffWords * sizeof(unsigned long long);
+    HIP_OK(hipMalloc(&ctx->d_handoff, bytes));
+    HIP_OK(hipMemset(ctx->d_handoff, 0, bytes));  // tag 0 never matches (blocks >= 1)
+    ctx->handoff_cap = n_px;
   }
   A.fpl = fpl;
-  A.progress = ctx->d_progress;
+  A.handoff = ctx->d_handoff;
   A.spill = ctx->d_spill;
-  if (ctx->stats_on) HIP_OK(hipMemsetAsync(ctx->d_stats, 0, 8 * sizeof(unsigned long long), st));
+  if (ctx->stats_on) HIP_OK(hipMemsetAsync(ctx->d_stats, 0, kStatSlots * sizeof(unsigned long long), st));
   HIP_OK(hipEventRecord(ctx->ev0, st));
   int launches = 0;
   if (tiles > 0 && p->frames > 0) {
-    HIP_OK(hipMemsetAsync(ctx->d_queue, 0, (size_t)n_launch * sizeof(uint32_t), st));
+    HIP_OK(hipMemsetAsync(ctx->d_queue, 0, (size_t)n_launch * kQueues * kQueueStride * sizeof(uint32_t), st));
     for (int64_t f0 = 0; f0 < p->frames; f0 += max_blocks * fpl) {
       A.frame_begin = p->frame_begin + (int32_t)f0;
       A.frames = (int32_t)std::min<int64_t>(max_blocks * fpl, p->frames - f0);
       A.blocks = (A.frames + fpl - 1) / fpl;
-      A.queue = ctx->d_queue + launches;
-      if (A.blocks > 1) HIP_OK(hipMemsetAsync(ctx->d_progress, 0, (size_t)n_px * sizeof(int32_t), st));
+      A.queue = ctx->d_queue + (size_t)launches * kQueues * kQueueStride;
+      // a fresh tag per launch: granules of earlier launches never match.
+      // After 2^20 launches the tags wrap; clear the granules then.
+      if (((++ctx->launch_seq) & 0xFFFFFu) == 0) {
+        ++ctx->launch_seq;
+        if (ctx->d_handoff)
+          HIP_OK(hipMemsetAsync(ctx->d_handoff, 0, (size_t)ctx->handoff_cap * kHandoffWords * 8, st));
+      }
+      A.tag_base = (ctx->launch_seq & 0xFFFFFu) << 12;
       void *kargs[] = {&A};
-      HIP_OK(hipLaunchKernel(kfn, dim3(grid), dim3(64), kargs, lds, st));
+      HIP_OK(hipLaunchKernel(kfn, dim3((unsigned)grid), dim3(64), kargs, lds, st));
       ++launches;
     }
   }
   HIP_OK(hipEventRecord(ctx->ev1, st));
-  HIP_OK(hipEventSynchronize(ctx->ev1));
-  float ms = 0.0f;
-  HIP_OK(hipEventElapsedTime(&ms, ctx->ev0, ctx->ev1));
+  // asynchronous: mcpt_get_stats waits for ev1 and reads the time and counters
   std::memset(&ctx->last, 0, sizeof(ctx->last));
-  ctx->last.kernel_ms = ms;
   ctx->last.launches = launches;
   ctx->last.frames_per_block = fpl;
-  if (ctx->stats_on) {
-    unsigned long long h[8];
-    HIP_OK(hipMemcpy(h, ctx->d_stats, sizeof(h), hipMemcpyDeviceToHost));
-    ctx->last.segments = h[0];
-    ctx->last.node_visits = h[1];
-    ctx->last.tri_tests = h[2];
-    ctx->last.bad_material = h[3];
-    ctx->last.wave_node_phases = h[4];
-    ctx->last.wave_leaf_phases = h[5];
-    ctx->last.wave_shade_phases = h[6];
-    ctx->last.order_fallbacks = h[7];
-  }
+  ctx->last.stack_window = win ? 1 : 0;
+  ctx->last.workgroups = (int32_t)grid;
+  ctx->last_pending = true;
+  ctx->last_stats = ctx->stats_on;
   return MCPT_OK;
 }
 

@@ -119,6 +119,23 @@ class Renderer:
         L.check(L.lib().mcpt_get_stats(self.ctx, ctypes.byref(s)))
         return {f: getattr(s, f) for f, _ in L.Stats._fields_ if f != "pad"}
 
+    def set_tuning(self, **knobs):
+        """mcpt_set_tuning: k_render launch-plan knobs (leaf_threshold,
+        shade_threshold, queue_chunk, block_entries, max_block_frames,
+        stack_window 0 auto / 1 window / 2 whole stack, lds_pad, queues); speed only,
+        unnamed knobs take their defaults."""
+        t = L.Tuning()
+        for k, v in knobs.items():
+            if k not in dict(L.Tuning._fields_):
+                raise L.MCPTError("unknown tuning knob %r" % k)
+            setattr(t, k, int(v))
+        L.check(L.lib().mcpt_set_tuning(self.ctx, ctypes.byref(t)))
+
+    def get_tuning(self):
+        t = L.Tuning()
+        L.check(L.lib().mcpt_get_tuning(self.ctx, ctypes.byref(t)))
+        return {f: getattr(t, f) for f, _ in L.Tuning._fields_}
+
     def selfcheck_trig(self):
         """(angle, range) mismatch counts of the inline randomDirection sin/cos
         against the ocml calls (mcpt_selfcheck_trig); (0, 0) on a good build."""
@@ -130,6 +147,12 @@ class Renderer:
         """Streaming HBM read bandwidth in GB/s (mcpt_measure_read_bw)."""
         g = ctypes.c_double()
         L.check(L.lib().mcpt_measure_read_bw(self.ctx, int(nbytes), ctypes.byref(g)))
+        return g.value
+
+    def gather_probe(self, record_bytes, table_bytes=1 << 31):
+        """Device ms of mcpt_gather_probe (the FETCH_SIZE calibration kernel)."""
+        g = ctypes.c_double()
+        L.check(L.lib().mcpt_gather_probe(self.ctx, int(record_bytes), int(table_bytes), ctypes.byref(g)))
         return g.value
 
     def new_state(self, width, height, seeds=None):
@@ -233,6 +256,12 @@ def build_hlbvh_device(tris, device=0):
     nodes = torch.empty((2 * n - 1) * L.BVHNODE.itemsize, dtype=torch.uint8, device=tris.device)
     L.check(L.lib().mcpt_build_hlbvh_device(L.ptr(tris), n, L.ptr(nodes), _stream()))
     return nodes
+
+
+def build_hlbvh_host_nodes(tris, device=0):
+    """HLBVH<CPU> nodes built on the GPU and returned as a host BVHNODE array
+    (bit-identical to scene.build_hlbvh; a `build` for SceneData.from_arrays)."""
+    return records(build_hlbvh_device(tris, device), L.BVHNODE).copy()
 
 
 def treelet_device(nodes, device=0):

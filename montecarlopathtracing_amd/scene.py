@@ -111,13 +111,15 @@ class SceneData:
         return cls(packed, build_hlbvh(packed), mats)
 
     @classmethod
-    def from_arrays(cls, verts, mat_index, mats):
-        """verts: (n, 3, 3) float32 triangle corners."""
+    def from_arrays(cls, verts, mat_index, mats, build=None):
+        """verts: (n, 3, 3) float32 triangle corners.  `build` makes the
+        HLBVH from the packed triangles (default: the host build_hlbvh;
+        render.build_hlbvh_host_nodes builds the same tree on the GPU)."""
         v = np.asarray(verts, np.float32)
         t = np.zeros(len(v), L.TRIANGLE)
         t["v"][:, :, :3] = v
         packed = pack_triangles(t, mat_index)
-        return cls(packed, build_hlbvh(packed), mats)
+        return cls(packed, (build or build_hlbvh)(packed), mats)
 
 
 def diffuse_only(mats):
@@ -134,7 +136,7 @@ def diffuse_only(mats):
 RANDOM_MESH_CAMERA = {"position": [50.0, 50.0, -150.0], "lookat": [50.0, 50.0, 50.0], "up": [0, 1, 0], "fov": 45.0}
 
 
-def random_mesh(n, seed=42, extent=100.0):
+def random_mesh(n, seed=42, extent=100.0, build=None):
     """BASELINE.json configs[4] / SURVEY.md §8(d) C5: n random triangles,
     centres uniform in [0, extent]^3, corners = centre + U[-h, h]^3 with
     h = 0.5 * extent / n^(1/3); diffuse 0.5; one emissive quad (Ka 10)
@@ -152,4 +154,4 @@ def random_mesh(n, seed=42, extent=100.0):
     mats = np.zeros(2, L.MATERIAL)
     mats[0] = classify_material(1.0, (0, 0, 0), (0.5, 0.5, 0.5), (0, 0, 0), 1.0)
     mats[1] = classify_material(1.0, (10, 10, 10), (0, 0, 0), (0, 0, 0), 1.0)
-    return SceneData.from_arrays(verts, mat_index, mats)
+    return SceneData.from_arrays(verts, mat_index, mats, build=build)

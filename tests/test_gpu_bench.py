@@ -38,8 +38,12 @@ def test_bench_two_ranks_rehearsal():
     lines = _lines(r.stdout)
     assert len(lines) == 1, r.stdout  # rank 0 only
     j = lines[0]
-    assert j["n_gpus"] == 2 and j["steps"] == 4 and j["scaling"] == "weak"
+    # headline: the fixed 1024x1024 image striped over the ranks (strong);
+    # the weak-scaled leg (a 1024x2048 image, 1024x1024 per rank) beside it
+    assert j["n_gpus"] == 2 and j["steps"] == 4 and j["scaling"] == "strong"
     assert j["value"] > 0 and j["config"]["parallelism"] == "row-stripe tiles x2"
+    assert j["config"]["width"] == 1024 and j["config"]["height"] == 1024
+    assert j["weak_scaling"]["value"] > 0 and j["weak_scaling"]["image"] == [1024, 2048]
     assert j["cpu_baseline"] is None  # rank 0 at N=1 only
     assert j["image_reduce_ms"] is not None and j["image_reduce_ms"] > 0  # the final image reduce ran
 
@@ -52,5 +56,24 @@ def test_bench_c4_strong_two_ranks_rehearsal():
                        capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stderr[-3000:]
     j = _lines(r.stdout)[0]
-    assert j["scaling"] == "strong" and j["config"]["height_per_gpu"] == 540
+    assert j["scaling"] == "strong" and j["config"]["height"] == 1080 and j["weak_scaling"] is None
     assert j["image_reduce_ms"] is not None
+
+
+def test_bench_default_line():
+    """The driver's own command at N = 1: the contract keys, a roofline whose
+    fractions are fractions, and the CPU baseline with its core count."""
+    r = subprocess.run([sys.executable, "bench.py", "--steps", "8", "--warmup", "2"], cwd=ROOT, capture_output=True,
+                       text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    j = _lines(r.stdout)[-1]
+    for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
+              "vs_baseline", "dtype", "data", "config", "roofline", "cpu_baseline"):
+        assert k in j, k
+    assert j["n_gpus"] == 1 and j["steps"] == 8 and j["value"] > 0
+    roof = j["roofline"]
+    assert roof["bound"] == "hbm" and roof["peak"] == 8000.0
+    for k in ("frac", "issue_frac"):
+        assert roof.get(k) is None or 0.0 <= roof[k] <= 1.0, (k, roof.get(k))
+    cpu = j["cpu_baseline"]
+    assert cpu["cores"] >= 1 and cpu["threads"] == cpu["cores"] and cpu["cpu_model"] and cpu["value"] > 0

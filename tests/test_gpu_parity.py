@@ -7,6 +7,8 @@ Only Hit.triangle_id is exempt in the pruned mode: it is the reference's
 "last accepted triangle" (objdef.h:262-265), which shade never reads; the
 NOPRUNE mode reproduces it too.
 """
+import functools
+
 import numpy as np
 import pytest
 
@@ -254,12 +256,15 @@ def test_frame_blocks_handoff_full_size(rnd):
 @pytest.mark.parametrize("name,getter,camjson,depth", [("cbox", scenes.cbox, scenes.CBOX_CAM, 8),
                                                        ("dining", scenes.dining, scenes.DINING_CAM, 16)])
 @pytest.mark.parametrize("schedule", [L.SCHED_SINGLE, L.SCHED_PAIRED])
-def test_render_windowed_stack_bitexact(rnd, monkeypatch, name, getter, camjson, depth, schedule):
+def test_render_windowed_stack_bitexact(rnd, name, getter, camjson, depth, schedule):
     """The LDS-window stack (top 32 entries in LDS, the rest spilled to a
     per-lane global area; picked at launch for deep trees) is the same
     logical stack: forced on, renders still match the reference bit for bit."""
-    monkeypatch.setenv("MCPT_STACK_WINDOW", "1")
-    (h_, c_, s_), (rh, rc, rs) = _render_both(rnd, getter(), camjson, 64, 64, depth, 4, 4, schedule=schedule)
+    rnd.set_tuning(stack_window=1)
+    try:
+        (h_, c_, s_), (rh, rc, rs) = _render_both(rnd, getter(), camjson, 64, 64, depth, 4, 4, schedule=schedule)
+    finally:
+        rnd.set_tuning()
     assert_bits_equal(c_, rc, "count")
     assert_bits_equal(s_, rs, "seeds")
     assert_bits_equal(h_, rh, "hist")
@@ -323,6 +328,62 @@ def test_render_edge_sizes_bitexact(rnd, w, h, depth, frames, attempt, schedule)
     assert_bits_equal(c_, rc, "count")
     assert_bits_equal(s_, rs, "seeds")
     assert_bits_equal(h_, rh, "hist")
+
+
+@functools.lru_cache(None)
+def _c5_small():
+    """C5's scene family (BASELINE.json configs[4], scene.random_mesh) at
+    500 K triangles: a deep random-soup HLBVH."""
+    return S.random_mesh(500_000, seed=7)
+
+
+@needs_ref
+@pytest.mark.parametrize("schedule", [L.SCHED_SINGLE, L.SCHED_PAIRED])
+def test_random_mesh_c5_bitexact(rnd, schedule):
+    """C5 (the deep-BVH random mesh): 500 K triangles at 64x64, depth 8, 5
+    frames, with the launch plan on auto (the stack layout picked by the
+    occupancy rule, not forced; 5 one-frame blocks handed between lanes).
+    The reference's own kernels traverse the same tree with their fixed
+    int stack[64] (objdef.h:247); images, counts and seeds match bit for
+    bit."""
+    data = _c5_small()
+    assert S.bvh_stack_depth(data.nodes) <= 64  # within the reference's stack
+    (h_, c_, s_), (rh, rc, rs) = _render_both(rnd, data, S.RANDOM_MESH_CAMERA, 64, 64, 8, 5, 4, schedule=schedule)
+    st = rnd.stats()
+    assert st["frames_per_block"] == 1 and st["stack_window"] in (0, 1)
+    assert_bits_equal(c_, rc, "count")
+    assert_bits_equal(s_, rs, "seeds")
+    assert_bits_equal(h_, rh, "hist")
+    assert (rc > 0).any()  # the light is seen through the soup
+
+
+def test_random_mesh_c5_full_size_properties(rnd):
+    """C5 at its full size: 10 M random triangles, the HLBVH built on the GPU
+    (mcpt_build_hlbvh_device), 2048x2048, depth 8, 2 frames.  Size-independent
+    properties: one 2-frame block, two 1-frame blocks handed between lanes,
+    and the rows split into 3 GPUs' stripes rendered in turn give the same
+    bits; radiance is finite and non-negative, counts are within [0, 2] and
+    some pixels see the light."""
+    data = S.random_mesh(10_000_000, build=R.build_hlbvh_host_nodes)
+    cam = S.parse_camera(S.RANDOM_MESH_CAMERA)
+    w = h = 2048
+    seeds = R.default_seeds(w * h)
+    dsc = rnd.upload(data)
+    outs = []
+    for stripes, fpl in ((1, 2), (1, 1), (3, 1)):
+        st = rnd.new_state(w, h, seeds)
+        for k in range(stripes):
+            rnd.render_frames(dsc, cam, st, 8, 1 << 20, 2, stripe_rows=16, stripe_index=k, stripe_count=stripes,
+                              frames_per_launch=fpl)
+        torch.cuda.synchronize()
+        outs.append((st.hist.cpu().numpy(), st.count.cpu().numpy(), st.seeds_np()))
+    dsc.close()
+    for o in outs[1:]:
+        for a, b, what in zip(outs[0], o, ("hist", "count", "seeds")):
+            assert_bits_equal(a, b, what)
+    hist, count = outs[0][0], outs[0][1]
+    assert np.isfinite(hist).all() and (hist >= 0).all()
+    assert count.min() >= 0 and count.max() <= 2 and (count > 0).sum() > 1000
 
 
 def test_render_zero_frames_and_bad_params(rnd):

@@ -1,0 +1,242 @@
+"""rocprofv3 evidence for bench.py's roofline, on the bench's own command.
+
+On the GPU box (one gpurun call; every pass is its own process under its own
+time limit, counters in separate --pmc passes as MI355X_MICROARCH.md asks):
+
+    python tools/profile.py run <tag> [bench args ...]     # e.g. r02 --steps 20 --warmup 5
+
+  gpurun_out/prof_<tag>/bench.json          the bench line of the exact command
+  gpurun_out/prof_<tag>/trace/              --kernel-trace --stats of the same command (--no-cpu)
+  gpurun_out/prof_<tag>/pmc_<pass>/         one --pmc pass each (PASSES below)
+  gpurun_out/prof_<tag>/calib_<pass>/       FETCH_SIZE / WRITE_SIZE of the gather-calibration
+                                            kernel (mcpt_gather_probe, 64- and 128-B records)
+
+Back here:
+
+    python tools/profile.py summarize <tag>
+
+copies the CSVs to profiles/<tag>_*.csv and writes profiles/<tag>_summary.json
+plus the entry of profiles/pmc_summary.json that bench.py reads (keyed by
+workload and frames per call).  The timed launch is the LAST dispatch of the
+bench's non-counting k_render instantiation (bench order: schedule tuning,
+warmup, timed call, then the counting replay with a different
+instantiation); its per-dispatch counters are the ones summarised.
+"""
+import csv
+import glob
+import json
+import os
+import re
+import shutil
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+# one rocprofv3 --pmc pass each (block limits: 8 SQ, 4 TCC with FETCH_SIZE=3
+# and WRITE_SIZE=2, 4 TCP, 2 GRBM)
+PASSES = {
+    "fetch": ["FETCH_SIZE"],
+    "write": ["WRITE_SIZE"],
+    "sq": ["SQ_WAVES", "SQ_WAVE_CYCLES", "SQ_BUSY_CYCLES", "SQ_ACTIVE_INST_VALU", "SQ_ACTIVE_INST_ANY",
+           "SQ_WAIT_ANY", "SQ_INSTS_VALU", "SQ_INSTS_VMEM_RD", "GRBM_GUI_ACTIVE"],
+    "sq2": ["SQ_INSTS_SALU", "SQ_INSTS_LDS", "SQ_INSTS_BRANCH", "SQ_ACTIVE_INST_LDS", "SQ_ACTIVE_INST_SCA",
+            "SQ_WAIT_INST_ANY", "SQ_THREAD_CYCLES_VALU", "SQ_INSTS_VMEM_WR", "GRBM_GUI_ACTIVE"],
+    "cache": ["TCC_HIT_sum", "TCC_MISS_sum", "TCP_TCC_READ_REQ_sum", "TCP_TOTAL_CACHE_ACCESSES_sum"],
+    "lat": ["TCP_TCP_LATENCY_sum", "TCP_TCC_READ_REQ_LATENCY_sum", "TA_TA_BUSY_sum", "TD_TD_BUSY_sum"],
+    "derived": ["VALUBusy", "VALUUtilization"],
+}
+HBM_PEAK_GBS = 8000.0
+N_CU = 256
+
+
+def sh(cmd, log, limit):
+    with open(log, "w") as fh:
+        r = subprocess.run(["timeout", "-k", "10", str(limit)] + cmd, stdout=fh, stderr=subprocess.STDOUT,
+                           cwd="/tmp", env=dict(os.environ, TMPDIR="/tmp"))
+    if r.returncode != 0:
+        print("FAILED (%d): %s\n%s" % (r.returncode, " ".join(cmd), open(log).read()[-3000:]), flush=True)
+        sys.exit(1)
+
+
+def run(tag, args):
+    out = os.path.join(ROOT, "gpurun_out", "prof_" + tag)
+    os.makedirs(out, exist_ok=True)
+    bench = [sys.executable, os.path.join(ROOT, "bench.py")] + args
+    print("bench:", " ".join(args), flush=True)
+    with open(os.path.join(out, "bench.json"), "w") as fh:
+        r = subprocess.run(["timeout", "-k", "10", "400"] + bench, stdout=fh, stderr=subprocess.PIPE, text=True)
+    if r.returncode != 0:
+        print(r.stderr[-3000:])
+        sys.exit(1)
+    line = open(os.path.join(out, "bench.json")).read().strip()
+    print(line[-600:], flush=True)
+    # the same command with the schedule the bench line's tuning picked, so
+    # every pass profiles the same kernel instantiation
+    sched = json.loads(line.splitlines()[-1])["config"]["schedule"]
+    quiet = bench + ["--no-cpu", "--schedule", sched]
+    sh(["rocprofv3", "--kernel-trace", "--stats", "--output-format", "csv", "-d", os.path.join(out, "trace"), "--"]
+       + quiet, os.path.join(out, "trace.log"), 400)
+    print("trace done", flush=True)
+    for name, ctrs in PASSES.items():
+        sh(["rocprofv3", "--pmc"] + ctrs + ["--output-format", "csv", "-d", os.path.join(out, "pmc_" + name), "--"]
+           + quiet, os.path.join(out, "pmc_%s.log" % name), 300)
+        print("pmc", name, "done", flush=True)
+    calib = [sys.executable, os.path.join(ROOT, "tools", "profile.py"), "calib"]
+    for name in ("fetch", "write"):
+        sh(["rocprofv3", "--pmc"] + PASSES[name] + ["--output-format", "csv", "-d", os.path.join(out, "calib_" + name),
+                                                    "--"] + calib, os.path.join(out, "calib_%s.log" % name), 200)
+    print("calibration done", flush=True)
+
+
+def calib():
+    """The calibration kernel alone (run under rocprofv3 by `run`)."""
+    sys.path.insert(0, ROOT)
+    from montecarlopathtracing_amd import render as R
+    rnd = R.Renderer(0)
+    for rec in (128, 64):
+        ms = rnd.gather_probe(rec, 1 << 31)
+        print("gather_probe %d-B records, 2 GiB table: %.3f ms = %.1f GB/s" % (rec, ms, (1 << 31) / ms / 1e6))
+
+
+def newest(pattern):
+    hits = sorted(glob.glob(pattern), key=os.path.getmtime)
+    if not hits:
+        raise SystemExit("missing: " + pattern)
+    return hits[-1]
+
+
+def dispatches(path, name_re):
+    """{dispatch_id: {counter: value, "kernel": name}} for kernels matching name_re."""
+    out = {}
+    for r in csv.DictReader(open(path)):
+        if re.search(name_re, r["Kernel_Name"]):
+            d = out.setdefault(int(r["Dispatch_Id"]), {"kernel": r["Kernel_Name"]})
+            d[r["Counter_Name"]] = float(r["Counter_Value"])
+    return out
+
+
+def summarize(tag):
+    src = os.path.join(ROOT, "gpurun_out", "prof_" + tag)
+    dst = os.path.join(ROOT, "profiles")
+    bench_line = open(os.path.join(src, "bench.json")).read().strip().splitlines()[-1]
+    bench = json.loads(bench_line)
+    shutil.copy(os.path.join(src, "bench.json"), os.path.join(dst, tag + "_bench.json"))
+    stats_csv = newest(os.path.join(src, "trace", "*", "*_kernel_stats.csv"))
+    trace_csv = newest(os.path.join(src, "trace", "*", "*_kernel_trace.csv"))
+    shutil.copy(stats_csv, os.path.join(dst, tag + "_kernel_stats.csv"))
+    shutil.copy(trace_csv, os.path.join(dst, tag + "_kernel_trace.csv"))
+    sched = bench["config"]["schedule"]
+    kname = r"k_render<0, false, (false|true), %s>" % ("true" if sched == "paired" else "false")
+    trace = [r for r in csv.DictReader(open(trace_csv)) if re.search(kname, r["Kernel_Name"])]
+    timed = trace[-1]
+    timed_ms = (int(timed["End_Timestamp"]) - int(timed["Start_Timestamp"])) / 1e6
+    same = [r for r in trace if r["Kernel_Name"] == timed["Kernel_Name"]]
+    stats = {r["Name"]: r for r in csv.DictReader(open(stats_csv))}
+    st = stats.get(timed["Kernel_Name"], {})
+    ctr = {}
+    for name in PASSES:
+        f = newest(os.path.join(src, "pmc_" + name, "*", "*_counter_collection.csv"))
+        shutil.copy(f, os.path.join(dst, "%s_pmc_%s.csv" % (tag, name)))
+        ds = dispatches(f, kname)
+        last = ds[max(ds)]  # the timed launch: the last dispatch of the instantiation
+        ctr.update({k: v for k, v in last.items() if k != "kernel"})
+    cal = {}
+    for name in ("fetch", "write"):
+        f = newest(os.path.join(src, "calib_" + name, "*", "*_counter_collection.csv"))
+        shutil.copy(f, os.path.join(dst, "%s_calib_%s.csv" % (tag, name)))
+        ds = dispatches(f, r"k_gather_probe")
+        ids = sorted(ds)  # run order: 128-B records, then 64-B
+        c = PASSES[name][0]
+        cal[name] = {"128": ds[ids[0]][c] * 1024.0, "64": ds[ids[1]][c] * 1024.0}
+    known = float(1 << 31)
+    # FETCH_SIZE scale for this kernel's gathers: known bytes / counted bytes
+    # of the calibration kernel, record sizes weighted as k_render reads them
+    # (128-B nodes and 64-B triangles per segment, from the bench's counters)
+    r = bench.get("roofline") or {}
+    n_node, n_tri = r.get("kernel_node_fetches_per_seg", 7.16), r.get("kernel_tri_tests_per_seg", 2.97)
+    s128, s64 = known / cal["fetch"]["128"], known / cal["fetch"]["64"]
+    w128 = 128.0 * n_node / (128.0 * n_node + 64.0 * n_tri)
+    fetch_scale = w128 * s128 + (1 - w128) * s64
+    rd_raw = ctr["FETCH_SIZE"] * 1024.0
+    wr = ctr["WRITE_SIZE"] * 1024.0
+    rd = rd_raw * fetch_scale
+    secs = timed_ms / 1e3
+    grbm = ctr["GRBM_GUI_ACTIVE"]  # summed over the 8 XCDs (MI355X_MICROARCH.md)
+    cycles = grbm / 8.0
+    l2_req = ctr["TCC_HIT_sum"] + ctr["TCC_MISS_sum"]
+    summ = {
+        "tag": tag, "command": "python3 bench.py " + " ".join(bench_args_of(bench)),
+        "workload": bench["config"]["workload"], "steps": bench["steps"], "warmup": bench["warmup"],
+        "frames_per_block": bench["config"].get("frames_per_block"),
+        "kernel": timed["Kernel_Name"], "timed_dispatch_id": int(timed["Dispatch_Id"]),
+        "timed_launch_ms_rocprof": round(timed_ms, 4),
+        "bench_avg_launch_ms": r.get("avg_launch_ms"),
+        "rocprof_stats_average_ms_all_dispatches_of_kernel": round(float(st.get("AverageNs", 0)) / 1e6, 4),
+        "dispatches_of_kernel": len(same),
+        "FETCH_SIZE_bytes_raw": rd_raw, "WRITE_SIZE_bytes": wr,
+        "fetch_scale_calibrated": round(fetch_scale, 4),
+        "calibration": {"known_bytes": known, "FETCH_SIZE_bytes_128B_records": cal["fetch"]["128"],
+                        "FETCH_SIZE_bytes_64B_records": cal["fetch"]["64"],
+                        "WRITE_SIZE_bytes_128B_records": cal["write"]["128"],
+                        "WRITE_SIZE_bytes_64B_records": cal["write"]["64"],
+                        "scale_128": round(s128, 4), "scale_64": round(s64, 4), "weight_128": round(w128, 4)},
+        "hbm_read_bytes": rd, "hbm_write_bytes": wr, "hbm_bytes": rd + wr,
+        "hbm_GBps": round((rd + wr) / secs / 1e9, 2), "hbm_frac": round((rd + wr) / secs / 1e9 / HBM_PEAK_GBS, 5),
+        "kernel_cycles": cycles, "clock_GHz": round(cycles / secs / 1e9, 3),
+        "valu_busy": round(ctr["SQ_ACTIVE_INST_VALU"] / (N_CU * cycles), 4),
+        "valu_busy_rocprof_derived": round(ctr.get("VALUBusy", float("nan")) / 100.0, 4),
+        "valu_utilization_lanes": round(ctr.get("VALUUtilization", float("nan")) / 100.0, 4),
+        "wave_issue_any_per_wave_cycle": round(ctr["SQ_ACTIVE_INST_ANY"] / ctr["SQ_WAVE_CYCLES"], 4),
+        "wave_wait_any_per_wave_cycle": round(ctr["SQ_WAIT_ANY"] / ctr["SQ_WAVE_CYCLES"], 4),
+        "waves_per_simd_avg": round(ctr["SQ_WAVE_CYCLES"] / (N_CU * 4 * cycles / 4.0), 3),
+        "valu_insts": ctr["SQ_INSTS_VALU"], "vmem_rd_insts": ctr["SQ_INSTS_VMEM_RD"],
+        "salu_insts": ctr.get("SQ_INSTS_SALU"), "lds_insts": ctr.get("SQ_INSTS_LDS"),
+        "l1_accesses": ctr["TCP_TOTAL_CACHE_ACCESSES_sum"], "l1_to_l2_reads": ctr["TCP_TCC_READ_REQ_sum"],
+        "l1_hit_rate": round(1 - ctr["TCP_TCC_READ_REQ_sum"] / max(ctr["TCP_TOTAL_CACHE_ACCESSES_sum"], 1), 4),
+        "l2_requests": l2_req, "l2_hit_rate": round(ctr["TCC_HIT_sum"] / max(l2_req, 1), 4),
+        "l2_hit_GBps_128B_lines": round(ctr["TCC_HIT_sum"] * 128.0 / secs / 1e9, 1),
+        "gather_latency_cycles_per_vmem_rd": round(ctr["TCP_TCP_LATENCY_sum"] / max(ctr["SQ_INSTS_VMEM_RD"], 1), 1),
+        "ta_busy_sum": ctr.get("TA_TA_BUSY_sum"), "td_busy_sum": ctr.get("TD_TD_BUSY_sum"),
+        "counters_timed_dispatch": ctr,
+        "sources": ["profiles/%s_%s.csv" % (tag, x) for x in
+                    ["kernel_stats", "kernel_trace"] + ["pmc_" + n for n in PASSES] + ["calib_fetch", "calib_write"]],
+        "note": "counters of the timed launch only (last dispatch of the bench's non-counting k_render); "
+                "GRBM_GUI_ACTIVE is summed over the 8 XCDs (cycles = /8); SQ_* cycle counters are quad-cycles; "
+                "valu_busy = SQ_ACTIVE_INST_VALU / (CUs x cycles) (rocprofv3's VALUBusy definition); "
+                "hbm bytes = FETCH_SIZE x calibrated scale + WRITE_SIZE (memory-side: Infinity-Cache hits included)",
+    }
+    with open(os.path.join(dst, tag + "_summary.json"), "w") as fh:
+        json.dump(summ, fh, indent=1)
+    key = "%s@%d" % (bench["config"]["workload"].split(":")[0], bench["steps"])
+    path = os.path.join(dst, "pmc_summary.json")
+    try:
+        allw = json.load(open(path))
+    except (OSError, ValueError):
+        allw = {}
+    allw = {k: v for k, v in allw.items() if "@" in k}  # drop the round-1 layout
+    allw[key] = {"hbm_bytes_per_launch": rd + wr, "hbm_read_bytes_per_launch": rd, "hbm_write_bytes_per_launch": wr,
+                 "fetch_scale_calibrated": summ["fetch_scale_calibrated"], "valu_busy": summ["valu_busy"],
+                 "wave_wait_any_per_wave_cycle": summ["wave_wait_any_per_wave_cycle"],
+                 "l2_hit_rate": summ["l2_hit_rate"], "l1_hit_rate": summ["l1_hit_rate"],
+                 "l2_hit_GBps_128B_lines": summ["l2_hit_GBps_128B_lines"],
+                 "gather_latency_cycles_per_vmem_rd": summ["gather_latency_cycles_per_vmem_rd"],
+                 "timed_launch_ms_rocprof": summ["timed_launch_ms_rocprof"], "frames_per_block": summ["frames_per_block"],
+                 "source": "profiles/%s_summary.json" % tag}
+    with open(path, "w") as fh:
+        json.dump(allw, fh, indent=1, sort_keys=True)
+    print(json.dumps(summ, indent=1))
+
+
+def bench_args_of(b):
+    return ["--gpus", str(b["n_gpus"]), "--steps", str(b["steps"]), "--warmup", str(b["warmup"])] + (
+        [] if b["config"]["workload"].startswith("C2") else ["--workload", b["config"]["workload"].split(":")[0]])
+
+
+if __name__ == "__main__":
+    if sys.argv[1] == "run":
+        run(sys.argv[2], sys.argv[3:])
+    elif sys.argv[1] == "calib":
+        calib()
+    else:
+        summarize(sys.argv[2])

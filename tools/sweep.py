@@ -1,0 +1,105 @@
+"""A/B sweeps of k_render launch-plan knobs (speed only; every setting gives
+the same bits) on one GPU.
+
+    python tools/sweep.py --workload C2 --frames 20 --reps 5 \
+        --grid "queue_chunk=4,8,16 block_entries=8,16" [--fpl 0,5,20] [--schedule paired]
+
+Every combination of the grid is timed `reps` times, interleaved round-robin
+(so clock drift hits all alike), on the bench's own scene/state setup; prints
+one line per combination: median kernel ms and nominal Msamples/s.  With
+--stats the kernel's counters (segments, node/tri per segment, SIMT
+efficiency per phase) of one extra call per combination are printed too.
+"""
+import argparse
+import itertools
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+import torch  # noqa: E402
+
+import bench  # noqa: E402
+from montecarlopathtracing_amd import _lib as L  # noqa: E402
+from montecarlopathtracing_amd import render as R  # noqa: E402
+from montecarlopathtracing_amd import scene as S  # noqa: E402
+
+
+def parse_grid(text):
+    axes = []
+    for part in (text or "").split():
+        k, vals = part.split("=")
+        axes.append([(k, int(v)) for v in vals.split(",")])
+    return [dict(c) for c in itertools.product(*axes)] if axes else [{}]
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--workload", default="C2", choices=sorted(bench.WORKLOADS))
+    ap.add_argument("--frames", type=int, default=20)
+    ap.add_argument("--reps", type=int, default=5)
+    ap.add_argument("--grid", default="")
+    ap.add_argument("--fpl", default="0", help="comma list of frames_per_launch values (0 = auto)")
+    ap.add_argument("--schedule", default="paired", choices=["single", "paired"])
+    ap.add_argument("--stats", action="store_true")
+    ap.add_argument("--json", default=None, help="append result lines to this file")
+    a = ap.parse_args()
+    wl = bench.WORKLOADS[a.workload]
+    w, h, depth = wl["w"], wl["h"], wl["depth"]
+    data, camj = bench.load_scene(a.workload)
+    cam = S.parse_camera(camj)
+    rnd = R.Renderer(0)
+    dsc = rnd.upload(data)
+    dsc.schedule = L.SCHED_PAIRED if a.schedule == "paired" else L.SCHED_SINGLE
+    st = rnd.new_state(w, h)
+    combos = [(fpl, g) for fpl in (int(x) for x in a.fpl.split(",")) for g in parse_grid(a.grid)]
+    times = {i: [] for i in range(len(combos))}
+    fpb = {}
+    for i, (fpl, g) in enumerate(combos):  # warm every variant once
+        rnd.set_tuning(**g)
+        rnd.render_frames(dsc, cam, st, depth, 1 << 30, min(a.frames, 4), frames_per_launch=fpl)
+    torch.cuda.synchronize()
+    for _ in range(a.reps):
+        for i, (fpl, g) in enumerate(combos):
+            rnd.set_tuning(**g)
+            rnd.render_frames(dsc, cam, st, depth, 1 << 30, a.frames, frames_per_launch=fpl)
+            s = rnd.stats()
+            times[i].append(s["kernel_ms"])
+            fpb[i] = s["frames_per_block"]
+    out = []
+    for i, (fpl, g) in enumerate(combos):
+        ts = sorted(times[i])
+        med = ts[len(ts) // 2]
+        rec = {"workload": a.workload, "frames": a.frames, "fpl": fpl, "fpb": fpb[i], "tuning": g,
+               "kernel_ms_median": round(med, 3), "kernel_ms_min": round(ts[0], 3),
+               "Msamples_s": round(w * h * a.frames * depth / (med / 1e3) / 1e6, 1)}
+        if a.stats:
+            rnd.set_tuning(**g)
+            rnd.set_stats(True)
+            rnd.render_frames(dsc, cam, st, depth, 1 << 30, a.frames, frames_per_launch=fpl)
+            c = rnd.stats()
+            rnd.set_stats(False)
+            seg = max(c["segments"], 1)
+            rec.update({"segments": c["segments"], "node_per_seg": round(c["node_visits"] / seg, 3),
+                        "tri_per_seg": round(c["tri_tests"] / seg, 3),
+                        "simt_T": round(c["node_visits"] / (64.0 * max(c["wave_node_phases"], 1)), 3),
+                        "simt_L": round(c["tri_tests"] / (64.0 * max(c["wave_leaf_phases"], 1)), 3),
+                        "simt_S": round(seg / (64.0 * max(c["wave_shade_phases"], 1)), 3),
+                        "waiting_frac": round(c["lane_waiting"] / (64.0 * max(c["wave_iterations"], 1)), 4),
+                        "idle_frac": round(c["lane_idle"] / (64.0 * max(c["wave_iterations"], 1)), 4),
+                        "iters_per_seg": round(c["wave_iterations"] * 64.0 / seg, 3)})
+        print(json.dumps(rec), flush=True)
+        out.append(rec)
+    if a.json:
+        with open(a.json, "a") as fh:
+            for r in out:
+                fh.write(json.dumps(r) + "\n")
+    rnd.set_tuning()
+    dsc.close()
+    rnd.close()
+
+
+if __name__ == "__main__":
+    main()
