@@ -117,6 +117,16 @@ def cpu_model():
     return "unknown"
 
 
+def cpu_quota():
+    """CPUs this process may keep busy: the cgroup v2 quota (cpu.max) when one
+    is set, else None."""
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        return None if q == "max" else max(1, int(int(q) // int(per)))
+    except (OSError, ValueError):
+        return None
+
+
 def cpu_baseline(data, cam, h_img, target_s=15.0):
     """The CPU oracle on a bounded sample: every k-th pixel of the same image,
     same depth, frames scaled so the sample takes ~target_s seconds, on every
@@ -125,10 +135,16 @@ def cpu_baseline(data, cam, h_img, target_s=15.0):
     if not O.available():
         return None
     try:
-        threads = len(os.sched_getaffinity(0))
+        affinity = len(os.sched_getaffinity(0))
     except AttributeError:
-        threads = os.cpu_count() or 1
-    threads = max(1, threads)
+        affinity = os.cpu_count() or 1
+    quota = cpu_quota()
+    omp = int(os.environ["OMP_NUM_THREADS"]) if os.environ.get("OMP_NUM_THREADS", "").isdigit() else None
+    # every core this process may run on, capped by its CPU share (the cgroup
+    # quota, or OMP_NUM_THREADS where the host sets the share that way): more
+    # OpenMP threads than the share only time-slice (on the 256-core GPU box
+    # with a 16-CPU share, 256 threads ran 1.7x slower than 16)
+    threads = max(1, min(affinity, quota or affinity, omp or affinity))
     seeds = default_seeds(W * h_img)
     stride = 61
     px = np.arange(0, W * h_img, stride, dtype=np.int32)
@@ -141,7 +157,8 @@ def cpu_baseline(data, cam, h_img, target_s=15.0):
     _, _, _, st = O.render(data, cam, W, h_img, DEPTH, frames, 1 << 20, seeds, pixels=px, threads=threads)
     dt = time.time() - t0
     return {"value": len(px) * frames * DEPTH / dt / 1e6, "unit": "Msamples/s", "cores": threads,
-            "kind": "port", "nproc": os.cpu_count(), "cpu_model": cpu_model(), "threads": threads,
+            "kind": "port", "nproc": os.cpu_count(), "affinity_cpus": affinity, "cgroup_cpu_quota": quota, "omp_num_threads_env": omp,
+            "cpu_model": cpu_model(), "threads": threads,
             "sample": "every %dth pixel (%d px) of the 1024x1024 C2 image x %d frames x depth %d, %.1f s; "
                       "oracle/mcpt_oracle.c exhaustive reference traversal, %d OpenMP threads" % (
                           stride, len(px), frames, DEPTH, dt, threads),
@@ -241,10 +258,12 @@ def main():
     fpb = kst["frames_per_block"]
 
     # replay the same frames with counters on (deterministic: same segments)
+    # (the counting kernel runs the replay's warmup too, so the timed launch
+    # stays the last dispatch of the non-counting kernel: tools/profile.py)
     st2 = rnd.new_state(W, h_img, seeds)
+    rnd.set_stats(True)
     if args.warmup > 0:
         rnd.render_frames(dsc, cam, st2, DEPTH, attempt, args.warmup, **kw)
-    rnd.set_stats(True)
     rnd.render_frames(dsc, cam, st2, DEPTH, attempt, args.steps, **kw)
     cst = rnd.stats()
     rnd.set_stats(False)

@@ -158,6 +158,9 @@ typedef struct mcpt_stats {
                                        claim pending, or the launch's tail)  */
   int32_t  stack_window;            /* 1: the last call ran the LDS-window stack */
   int32_t  workgroups;              /* 64-lane workgroups per launch (resident grid) */
+  uint64_t debug_violations;        /* MCPT_DEBUG builds: stack-bound, node- and
+                                       triangle-index violations k_render caught
+                                       (always 0 in release builds)           */
 } mcpt_stats;
 
 /* Launch-plan knobs of the fused kernel (speed only: every setting gives the
@@ -225,7 +228,8 @@ int mcpt_bvh_sah(const mcpt_bvh_node *nodes, int64_t n_nodes, double *sah);
  * stbi_write_hdr with vertical flip, 4 components in, RGB out.           */
 int mcpt_write_hdr(const char *path, int32_t width, int32_t height,
                    const float *rgba, int32_t flip_vertically);
-/* Same encoder into memory: returns the byte count (call with NULL first). */
+/* Same encoder into memory: returns the byte count (call with NULL first);
+ * MCPT_ERR_ARG if `cap` is too small for it.                              */
 int64_t mcpt_encode_hdr(int32_t width, int32_t height, const float *rgba,
                         int32_t flip_vertically, uint8_t *out, int64_t cap);
 

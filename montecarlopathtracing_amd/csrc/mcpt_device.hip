@@ -38,7 +38,10 @@ using namespace mcpt;
 #ifndef MCPT_WAVES_PER_SIMD
 #define MCPT_WAVES_PER_SIMD 4  // k_render occupancy target (tools/sweep_waves.sh)
 #endif
-constexpr int kStackWindow = 32;  // k_render's LDS window when the whole stack would cost occupancy
+#ifndef MCPT_STACK_WINDOW_K
+#define MCPT_STACK_WINDOW_K 32
+#endif
+constexpr int kStackWindow = MCPT_STACK_WINDOW_K;  // k_render's LDS window when the whole stack would cost occupancy
 
 namespace mcpt {
 int fail(int code, const std::string &msg);  // mcpt_host.cpp
@@ -84,6 +87,8 @@ constexpr int32_t kEmptySlot = INT32_MIN + 2;  // unused 4-wide slot
 static_assert(kEmptySlot == mcpt::kEmptySlot4, "one empty-slot marker");
 
 struct SceneView {
+  int32_t n_near4, n_nodes4, n_int;  // record counts (bounds of the MCPT_DEBUG checks)
+  int64_t n_tris;
   const DevNode4 *near4;   // EXACT search tree (binned SAH, nearest-first; mcpt_sah.cpp)
   const DevNode4 *nodes4;  // the reference HLBVH collapsed 4-wide (left-first fallback)
   const DevNode *nodes;
@@ -113,6 +118,20 @@ constexpr int kQueues = 8;         // k_render work queues (at most): one per XC
 constexpr int kQueueStride = 32;   // u32 words between queue heads: one 128-B line each
 constexpr int kHandoffWords = 6;   // seed, mean.xyzw, count: one tagged 8-B granule each
 constexpr int kStatSlots = 16;     // k_render counters (mcpt_stats)
+constexpr int kDebugSlot = 12;     // MCPT_DEBUG: violations of the stack bound, node and triangle indices
+
+// -DMCPT_DEBUG (make debug -> lib/libmcpt_hip_debug.so): k_render checks every
+// stack push against its capacity and every node / triangle index against
+// its array before use, counts violations (mcpt_stats.debug_violations) and
+// skips the bad access instead of faulting.  The reference's own traversal
+// has an unchecked int stack[64] (objdef.h:247).
+#ifdef MCPT_DEBUG
+constexpr bool kDebug = true;
+#define MCPT_DCHECK(cond, slot) (__builtin_expect(!(cond), 0) ? (atomicAdd(&A.stats[kDebugSlot + (slot)], 1ull), false) : true)
+#else
+constexpr bool kDebug = false;
+#define MCPT_DCHECK(cond, slot) true
+#endif
 
 struct mcpt_ctx {
   int device;
@@ -652,6 +671,8 @@ __global__ void __launch_bounds__(64, MCPT_WAVES_PER_SIMD) k_render(RenderArgs A
   else
     stk = Stack{lds_stack + lane, 64};
   const SceneView &S = A.S;
+  const int stack_cap = WIN ? kStackWindow + A.spill_stride : A.stack_depth;  // entries (MCPT_DEBUG bound)
+  (void)stack_cap;
   // material table copied to LDS behind the stack (small tables only)
   const mcpt_material *mats = S.mats;
   if (A.lds_mats) {
@@ -822,10 +843,15 @@ __global__ void __launch_bounds__(64, MCPT_WAVES_PER_SIMD) k_render(RenderArgs A
         if (!LIT) {  // EXACT: SAH tree nearest-first, or the reference tree left-first
           uint32_t ctr = 0;
           const DevNode4 *__restrict__ tree = ref ? S.nodes4 : S.near4;
-          cur = step4<PRUNE>(tree[cur], o.xyz, rinv, kTmin, best_t + S.prune_margin, !ref, stk, sp, ctr);
+          if (MCPT_DCHECK(cur < (ref ? S.n_nodes4 : S.n_near4), 1)) {
+            cur = step4<PRUNE>(tree[cur], o.xyz, rinv, kTmin, best_t + S.prune_margin, !ref, stk, sp, ctr);
+            if (!MCPT_DCHECK(sp <= stack_cap, 0)) sp = stack_cap;
+          } else {
+            cur = kPop;
+          }
           if (STATS) n_nodes += ctr;
         } else {  // NOPRUNE: the reference's binary tree, literal division
-          const DevNode N = S.nodes[cur];
+          const DevNode N = S.nodes[MCPT_DCHECK(cur < S.n_int, 1) ? cur : 0];
           if (STATS) n_nodes++;
           BoxT bl, br;
           child_boxes<LIT>(N, o.xyz, d.xyz, rinv, bl, br);
@@ -837,6 +863,7 @@ __global__ void __launch_bounds__(64, MCPT_WAVES_PER_SIMD) k_render(RenderArgs A
           }
           if (hl && hr) stk.push(sp, N.right);  // push right, descend left
           cur = hl ? N.left : (hr ? N.right : kPop);
+          if (!MCPT_DCHECK(sp <= stack_cap, 0)) sp = stack_cap;
         }
         if (cur == kPop) cur = sp == 0 ? kDone : stk.pop(sp);
       }
@@ -852,9 +879,9 @@ __global__ void __launch_bounds__(64, MCPT_WAVES_PER_SIMD) k_render(RenderArgs A
         // the lane's sequence of tests is unchanged, one phase serves two leaves
         const int32_t nx = !PAIR || sp == 0 ? kDone : stk.peek(sp);
         const bool two = PAIR && nx < 0 && nx != kDone;
-        const DevTri T = S.tris[~cur];
+        const DevTri T = S.tris[MCPT_DCHECK(~cur < S.n_tris, 2) ? ~cur : 0];
         DevTri T2;
-        if (two) T2 = S.tris[~nx];
+        if (two) T2 = S.tris[MCPT_DCHECK(~nx < S.n_tris, 2) ? ~nx : 0];
         auto test = [&](const DevTri &X) {
           TriHit h = LIT ? cramer(d.xyz, X.nab.xyz, X.nac.xyz, X.v0.xyz - o.xyz, X.nrm.xyz, kTmin)
                          : cramer_reduced(d.xyz, X.nab.xyz, X.nac.xyz, X.v0.xyz - o.xyz, X.nrm.xyz, X.v0.w,
@@ -1046,7 +1073,7 @@ __global__ void k_accumulate(f4 *colors, f4 *hist, int32_t *count, int64_t n, in
 // =================================================================== ABI
 extern "C" {
 
-const char *mcpt_version(void) { return "mcpt-mi355x 0.1 (gfx950)"; }
+const char *mcpt_version(void) { return kDebug ? "mcpt-mi355x 0.2 (gfx950, MCPT_DEBUG)" : "mcpt-mi355x 0.2 (gfx950)"; }
 
 int mcpt_device_count(int32_t *count) {
   if (!count) return mcpt::fail(MCPT_ERR_ARG, "device_count: null");
@@ -1244,6 +1271,7 @@ int mcpt_get_stats(mcpt_ctx *c, mcpt_stats *out) {
       c->last.wave_iterations = h[8];
       c->last.lane_waiting = h[9];
       c->last.lane_idle = h[10];
+      c->last.debug_violations = h[kDebugSlot] + h[kDebugSlot + 1] + h[kDebugSlot + 2];
     }
   }
   *out = c->last;
@@ -1486,6 +1514,10 @@ int mcpt_scene_upload(mcpt_ctx *ctx, const mcpt_triangle *tris, int64_t n_tris, 
   s->stack_depth = std::max(depth, 1);
   s->stack_depth4 = depth4;
   SceneView &v = s->view;
+  v.n_near4 = (int32_t)near.size();
+  v.n_nodes4 = (int32_t)dn4.size();
+  v.n_int = (int32_t)dn.size();
+  v.n_tris = n;
   v.nodes = s->nodes;
   v.nodes4 = s->nodes4;
   v.near4 = s->near4;
@@ -1596,7 +1628,11 @@ int mcpt_render_frames(mcpt_ctx *ctx, const mcpt_scene *scene, const mcpt_camera
   const size_t lds_win = (size_t)kStackWindow * 64 * sizeof(int32_t) + lds_mats + pad;
   bool win = false;
   int per_cu = 0;
-  if (depth_entries > kStackWindow && T.stack_window != 2) {
+  if (T.stack_window == 1) {  // forced (tests, experiments): the window even when the whole stack fits in it
+    win = true;
+    rc = occupancy(ctx, kfns[noprune][ctx->stats_on][1][pair], lds_win, &per_cu);
+    if (rc) return rc;
+  } else if (depth_entries > kStackWindow && T.stack_window != 2) {
     int per_cu_plain = 0, per_cu_win = 0;
     rc = occupancy(ctx, kfns[noprune][ctx->stats_on][0][pair], lds_plain, &per_cu_plain);
     if (rc) return rc;
@@ -1611,7 +1647,7 @@ int mcpt_render_frames(mcpt_ctx *ctx, const mcpt_scene *scene, const mcpt_camera
   const size_t lds = win ? lds_win : lds_plain;
   const void *kfn = kfns[noprune][ctx->stats_on][win][pair];
   A.stack_depth = win ? kStackWindow : depth_entries;  // the material table follows the stack in LDS
-  A.spill_stride = win ? depth_entries - kStackWindow : 0;
+  A.spill_stride = win ? std::max(0, depth_entries - kStackWindow) : 0;
   const int64_t grid = std::max<int64_t>(1, std::min<int64_t>(tiles, (int64_t)std::max(per_cu, 1) * ctx->n_cu));
   const int64_t spill_need = win ? grid * 64 * (int64_t)A.spill_stride : 0;
   if (win && spill_need > ctx->spill_cap) {
@@ -1668,7 +1704,7 @@ int mcpt_render_frames(mcpt_ctx *ctx, const mcpt_scene *scene, const mcpt_camera
   A.fpl = fpl;
   A.handoff = ctx->d_handoff;
   A.spill = ctx->d_spill;
-  if (ctx->stats_on) HIP_OK(hipMemsetAsync(ctx->d_stats, 0, kStatSlots * sizeof(unsigned long long), st));
+  if (ctx->stats_on || kDebug) HIP_OK(hipMemsetAsync(ctx->d_stats, 0, kStatSlots * sizeof(unsigned long long), st));
   HIP_OK(hipEventRecord(ctx->ev0, st));
   int launches = 0;
   if (tiles > 0 && p->frames > 0) {
@@ -1699,7 +1735,7 @@ int mcpt_render_frames(mcpt_ctx *ctx, const mcpt_scene *scene, const mcpt_camera
   ctx->last.stack_window = win ? 1 : 0;
   ctx->last.workgroups = (int32_t)grid;
   ctx->last_pending = true;
-  ctx->last_stats = ctx->stats_on;
+  ctx->last_stats = ctx->stats_on || kDebug;
   return MCPT_OK;
 }
 

@@ -665,7 +665,9 @@ extern "C" int64_t mcpt_encode_hdr(int32_t width, int32_t height, const float *r
                                    uint8_t *out, int64_t cap) {
   if (width <= 0 || height <= 0 || !rgba) return fail(MCPT_ERR_ARG, "encode_hdr: bad argument");
   Sink s{out, cap, 0};
-  return encode_hdr(s, width, height, rgba, flip);
+  const int64_t n = encode_hdr(s, width, height, rgba, flip);
+  if (out && n > cap) return fail(MCPT_ERR_ARG, "encode_hdr: output buffer too small");
+  return n;
 }
 
 extern "C" int mcpt_write_hdr(const char *path, int32_t width, int32_t height, const float *rgba,

@@ -113,7 +113,7 @@ struct Builder {
     const int64_t mid = split(lo, hi);
     const int64_t lbase = base + 1, rbase = base + 2 * (mid - lo);
     // the two halves touch disjoint idx ranges and node ranges: safe to run in parallel
-    if ((1 << (depth + 1)) <= max_threads && hi - lo > 65536) {
+    if (depth < 16 && (1 << (depth + 1)) <= max_threads && hi - lo > 65536) {  // depth bound: no shift overflow (UBSan)
       std::thread t([&] { build(lo, mid, lbase, depth + 1); });
       build(mid, hi, rbase, depth + 1);
       t.join();

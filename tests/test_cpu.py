@@ -468,3 +468,22 @@ def test_diningroom_proxy_is_regenerated_bit_for_bit(tmp_path, monkeypatch):
     assert 90_000 < len(tris) < 110_000
     assert sorted(set(mats["type"].tolist())) == [L.MCPT_DIFFUSE, L.MCPT_GLOSSY, L.MCPT_LIGHT]
     assert (idx >= 0).all()
+
+
+# ------------------------------------------------------------- sanitizers
+@pytest.mark.parametrize("variant", ["host_asan", "host_tsan"])
+def test_host_code_under_sanitizers(variant):
+    """The host half of libmcpt_hip.so (csrc/mcpt_host.cpp: loader, packing,
+    HLBVH, stack depth, SAH metric, camera, classification, RGBE writer;
+    csrc/mcpt_sah.cpp: the multi-threaded SAH search-tree builder) on the
+    committed scenes, synthetic meshes and edge cases, built with
+    AddressSanitizer + UndefinedBehaviorSanitizer (no recovery) and with
+    ThreadSanitizer (tests/native/host_sanitize.cpp)."""
+    import subprocess
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    native = os.path.join(root, "tests", "native")
+    subprocess.run(["make", "-s", "-C", native, variant], check=True, capture_output=True, timeout=300)
+    env = dict(os.environ, ASAN_OPTIONS="detect_leaks=1:abort_on_error=0", TSAN_OPTIONS="halt_on_error=1")
+    r = subprocess.run([os.path.join(native, variant), root, "8"], capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode == 0 and r.stdout.strip().endswith("0 failures"), r.stdout[-2000:] + r.stderr[-4000:]
+    assert "runtime error" not in r.stderr and "WARNING: ThreadSanitizer" not in r.stderr, r.stderr[-4000:]

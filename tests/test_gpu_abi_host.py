@@ -1,0 +1,97 @@
+"""The drop-in boundary exercised from C++: tests/native/abi_host.cpp is the
+reference's OpenCL::init/update + ColorOut loop (MCPT/OpenCLApp.cpp:36-82,
+colorout.cpp:55-68) written against include/mcpt_hip.h and linked with
+libmcpt_hip.so alone (no Python, no torch, no HIP headers).  It reads the
+reference-format config.json, renders one frame per update() call as the
+reference does, and dumps <objname>.hdr after attempt+1 frames.
+
+Bar: bit-exact.  After 16 updates of config 2 (C1: cbox 256x256, depth 4,
+attempt 16) with the golden seeds, the image, counts and seed chains equal
+the golden vectors the reference's own kernels produced; the .hdr it dumps
+after the 17th update equals stb's encoding of the reference kernels' 17-frame
+image."""
+import json
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+from montecarlopathtracing_amd import scene as S  # noqa: E402
+
+from . import refgpu, scenes  # noqa: E402
+
+ROOT = scenes.ROOT
+EXE = os.path.join(ROOT, "tests", "native", "abi_host")
+needs_exe = pytest.mark.skipif(not os.path.exists(EXE), reason="tests/native/abi_host not built (__graft_entry__.build)")
+
+
+def gold(name):
+    return np.load(os.path.join(ROOT, "tests", "golden", name))
+
+
+def _run(tmp_path, configid, seeds, *extra):
+    seed_file = "-"
+    if seeds is not None:
+        seed_file = str(tmp_path / "seeds.u32")
+        np.ascontiguousarray(seeds, np.uint32).tofile(seed_file)
+    r = subprocess.run([EXE, scenes.CFG, str(configid), seed_file, str(tmp_path)] + [str(x) for x in extra],
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    return json.loads(r.stdout.strip().splitlines()[-1])
+
+
+def _state(tmp_path, w, h):
+    raw = np.fromfile(str(tmp_path / "state.bin"), np.uint8)
+    n = w * h
+    hist = raw[:16 * n].view(np.float32).reshape(n, 4)
+    count = raw[16 * n:20 * n].view(np.int32)
+    seeds = raw[20 * n:24 * n].view(np.uint32)
+    return hist, count, seeds
+
+
+@needs_exe
+def test_cpp_host_c1_bitexact(tmp_path):
+    g = gold("image_c1_cbox.npz")
+    w, h, depth, frames, att = (int(x) for x in g["meta"])
+    out = _run(tmp_path, 2, g["seeds_in"], "--updates", frames)
+    assert out["frames_done"] == frames and out["dumped"] == ""  # 16 frames <= attempt: no dump yet
+    hist, count, seeds = _state(tmp_path, w, h)
+    assert np.array_equal(count, g["count"])
+    assert np.array_equal(seeds, g["seeds"])
+    assert hist.tobytes() == np.ascontiguousarray(g["hist"], np.float32).tobytes()
+
+
+@needs_exe
+@pytest.mark.skipif(not refgpu.available(), reason="oracle/_ref not built")
+def test_cpp_host_dump_equals_reference_hdr(tmp_path):
+    g = gold("image_c1_cbox.npz")
+    w, h, depth, frames, att = (int(x) for x in g["meta"])
+    out = _run(tmp_path, 2, g["seeds_in"])  # attempt + 1 = 17 updates, then the dump
+    assert out["frames_done"] == att + 1 and os.path.basename(out["dumped"]) == "cbox.obj.hdr"
+    ref_hist, ref_count, ref_seeds = refgpu.render(scenes.cbox(), S.parse_camera(scenes.CBOX_CAM), w, h, depth,
+                                                   att + 1, att, g["seeds_in"])
+    hist, count, seeds = _state(tmp_path, w, h)
+    assert np.array_equal(count, ref_count) and np.array_equal(seeds, ref_seeds)
+    assert hist.tobytes() == ref_hist.tobytes()
+    assert open(out["dumped"], "rb").read() == S.encode_hdr(ref_hist.reshape(h, w, 4))
+
+
+@needs_exe
+def test_cpp_host_batched_updates_equal_single_frames(tmp_path):
+    """Frames per update() call change nothing: 20 one-frame updates vs 4
+    updates of 5 frames (the dump after frame attempt+1 happens in both)."""
+    g = gold("image_c1_cbox.npz")
+    w, h = int(g["meta"][0]), int(g["meta"][1])
+    a, b = tmp_path / "a", tmp_path / "b"
+    a.mkdir()
+    b.mkdir()
+    oa = _run(a, 2, g["seeds_in"], "--updates", 20)
+    ob = _run(b, 2, g["seeds_in"], "--frames-per-update", 5, "--updates", 4)
+    assert oa["frames_done"] == ob["frames_done"] == 20 and oa["dumped"] and ob["dumped"]
+    ha, ca, sa = _state(a, w, h)
+    hb, cb, sb = _state(b, w, h)
+    assert ha.tobytes() == hb.tobytes() and np.array_equal(ca, cb) and np.array_equal(sa, sb)
+    assert int(ca.max()) <= 16  # MAX_ATTEMPT caps the count

@@ -29,7 +29,7 @@ def child(a):
     cam = S.parse_camera(camj)
     rnd = R.Renderer(0)
     dsc = rnd.upload(data)
-    dsc.schedule = L.SCHED_PAIRED
+    dsc.schedule = L.SCHED_PAIRED if a.schedule == "paired" else L.SCHED_SINGLE
     st = rnd.new_state(wl["w"], wl["h"])
     rnd.render_frames(dsc, cam, st, wl["depth"], 1 << 30, 4, frames_per_launch=a.fpl)
     ms = []
@@ -47,6 +47,7 @@ def main():
     ap.add_argument("--fpl", type=int, default=0)
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--schedule", default="paired", choices=["single", "paired"])
     ap.add_argument("--child", action="store_true")
     a = ap.parse_args()
     if a.child:
@@ -58,6 +59,7 @@ def main():
             env = dict(os.environ, MCPT_LIB_OVERRIDE=os.path.abspath(lib))
             out = subprocess.run([sys.executable, os.path.abspath(__file__), "--child", "--libs", lib,
                                   "--workload", a.workload, "--frames", str(a.frames), "--fpl", str(a.fpl),
+                                  "--schedule", a.schedule,
                                   "--reps", str(a.reps)], env=env, capture_output=True, text=True, timeout=600)
             line = [x for x in out.stdout.splitlines() if x.startswith("AB_RESULT ")]
             if out.returncode != 0 or not line:
@@ -68,6 +70,7 @@ def main():
     for lib in libs:
         ts = sorted(res[lib])
         print(json.dumps({"lib": os.path.basename(lib), "workload": a.workload, "frames": a.frames, "fpl": a.fpl,
+                          "schedule": a.schedule,
                           "kernel_ms_median": round(ts[len(ts) // 2], 3), "kernel_ms_min": round(ts[0], 3),
                           "n": len(ts)}), flush=True)
 
