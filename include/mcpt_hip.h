@@ -161,6 +161,9 @@ typedef struct mcpt_stats {
   uint64_t debug_violations;        /* MCPT_DEBUG builds: stack-bound, node- and
                                        triangle-index violations k_render caught
                                        (always 0 in release builds)           */
+  uint64_t phase_ticks[4];          /* MCPT_PHASE_TIMING builds: shader-clock ticks
+                                       all waves spent in fetch, T, L, S (0 in
+                                       release builds)                        */
 } mcpt_stats;
 
 /* Launch-plan knobs of the fused kernel (speed only: every setting gives the

@@ -48,7 +48,7 @@ class Stats(ctypes.Structure):
                 ("wave_shade_phases", ctypes.c_uint64), ("order_fallbacks", ctypes.c_uint64),
                 ("wave_iterations", ctypes.c_uint64), ("lane_waiting", ctypes.c_uint64), ("lane_idle", ctypes.c_uint64),
                 ("stack_window", ctypes.c_int32), ("workgroups", ctypes.c_int32),
-                ("debug_violations", ctypes.c_uint64)]
+                ("debug_violations", ctypes.c_uint64), ("phase_ticks", ctypes.c_uint64 * 4)]
 
 
 class Tuning(ctypes.Structure):

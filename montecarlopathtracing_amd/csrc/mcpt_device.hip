@@ -117,7 +117,8 @@ struct mcpt_scene {
 constexpr int kQueues = 8;         // k_render work queues (at most): one per XCD (MI355X has 8)
 constexpr int kQueueStride = 32;   // u32 words between queue heads: one 128-B line each
 constexpr int kHandoffWords = 6;   // seed, mean.xyzw, count: one tagged 8-B granule each
-constexpr int kStatSlots = 16;     // k_render counters (mcpt_stats)
+constexpr int kStatSlots = 24;     // k_render counters (mcpt_stats)
+constexpr int kPhaseSlot = 16;     // MCPT_PHASE_TIMING: shader-clock ticks per phase (fetch, T, L, S)
 constexpr int kDebugSlot = 12;     // MCPT_DEBUG: violations of the stack bound, node and triangle indices
 
 // -DMCPT_DEBUG (make debug -> lib/libmcpt_hip_debug.so): k_render checks every
@@ -125,6 +126,23 @@ constexpr int kDebugSlot = 12;     // MCPT_DEBUG: violations of the stack bound,
 // its array before use, counts violations (mcpt_stats.debug_violations) and
 // skips the bad access instead of faulting.  The reference's own traversal
 // has an unchecked int stack[64] (objdef.h:247).
+// -DMCPT_PHASE_TIMING (make timing -> lib/libmcpt_hip_timing.so): every wave
+// adds the shader-clock ticks (s_memtime) it spends in each phase of its loop
+// (fetch, T, L, S) to mcpt_stats.phase_ticks: where a wave's time goes,
+// latency included.  Diagnostics only; the reads cost time themselves.
+#ifdef MCPT_PHASE_TIMING
+constexpr bool kTiming = true;
+#define MCPT_TICK(k)                                            \
+  do {                                                          \
+    const uint64_t now_ = __builtin_amdgcn_s_memtime();         \
+    ph[k] += now_ - tick;                                       \
+    tick = now_;                                                \
+  } while (0)
+#else
+constexpr bool kTiming = false;
+#define MCPT_TICK(k) do {} while (0)
+#endif
+
 #ifdef MCPT_DEBUG
 constexpr bool kDebug = true;
 #define MCPT_DCHECK(cond, slot) (__builtin_expect(!(cond), 0) ? (atomicAdd(&A.stats[kDebugSlot + (slot)], 1ull), false) : true)
@@ -740,6 +758,10 @@ __global__ void __launch_bounds__(64, MCPT_WAVES_PER_SIMD) k_render(RenderArgs A
   uint32_t qs = (xcc_id() % nq) * 0x11u;
   uint32_t pool = 0, pool_left = 0;  // wave-uniform: claimed, unassigned entries of queue (qs >> 4) & 15
 
+#ifdef MCPT_PHASE_TIMING
+  uint64_t ph[4] = {0, 0, 0, 0};
+  uint64_t tick = __builtin_amdgcn_s_memtime();
+#endif
   for (;;) {
     // ---- fetch: lanes without work take the next queue entries, from the
     // wave's pool of claimed entries; one atomic claims max(chunk, shortfall)
@@ -828,6 +850,7 @@ __global__ void __launch_bounds__(64, MCPT_WAVES_PER_SIMD) k_render(RenderArgs A
         }
       }
     }
+    MCPT_TICK(0);
     if (!__ballot(lst != kDead)) break;
     const bool live = lst == kBusy;
     if (STATS) {
@@ -868,6 +891,7 @@ __global__ void __launch_bounds__(64, MCPT_WAVES_PER_SIMD) k_render(RenderArgs A
         if (cur == kPop) cur = sp == 0 ? kDone : stk.pop(sp);
       }
     }
+    MCPT_TICK(1);
     // ---- L: triangle tests, batched
     const bool in_l = live && cur < 0 && cur != kDone;
     const unsigned long long ml = __ballot(in_l);
@@ -904,6 +928,7 @@ __global__ void __launch_bounds__(64, MCPT_WAVES_PER_SIMD) k_render(RenderArgs A
         cur = sp == 0 ? kDone : stk.pop(sp);
       }
     }
+    MCPT_TICK(2);
     // ---- S: finish the segment (shade.cl), accumulate (history.cl), next segment
     const bool in_s = live && cur == kDone;
     const unsigned long long ms = __ballot(in_s);
@@ -966,7 +991,12 @@ __global__ void __launch_bounds__(64, MCPT_WAVES_PER_SIMD) k_render(RenderArgs A
         if (lst == kBusy) begin_segment();
       }
     }
+    MCPT_TICK(3);
   }
+#ifdef MCPT_PHASE_TIMING
+  if (lane == 0)
+    for (int k = 0; k < 4; ++k) atomicAdd(&A.stats[kPhaseSlot + k], (unsigned long long)ph[k]);
+#endif
   if (STATS) {
     atomicAdd(&A.stats[0], n_seg);
     atomicAdd(&A.stats[1], n_nodes);
@@ -1073,7 +1103,10 @@ __global__ void k_accumulate(f4 *colors, f4 *hist, int32_t *count, int64_t n, in
 // =================================================================== ABI
 extern "C" {
 
-const char *mcpt_version(void) { return kDebug ? "mcpt-mi355x 0.2 (gfx950, MCPT_DEBUG)" : "mcpt-mi355x 0.2 (gfx950)"; }
+const char *mcpt_version(void) {
+  return kDebug ? "mcpt-mi355x 0.2 (gfx950, MCPT_DEBUG)"
+                : (kTiming ? "mcpt-mi355x 0.2 (gfx950, MCPT_PHASE_TIMING)" : "mcpt-mi355x 0.2 (gfx950)");
+}
 
 int mcpt_device_count(int32_t *count) {
   if (!count) return mcpt::fail(MCPT_ERR_ARG, "device_count: null");
@@ -1272,6 +1305,7 @@ int mcpt_get_stats(mcpt_ctx *c, mcpt_stats *out) {
       c->last.lane_waiting = h[9];
       c->last.lane_idle = h[10];
       c->last.debug_violations = h[kDebugSlot] + h[kDebugSlot + 1] + h[kDebugSlot + 2];
+      for (int k = 0; k < 4; ++k) c->last.phase_ticks[k] = h[kPhaseSlot + k];
     }
   }
   *out = c->last;
@@ -1661,10 +1695,16 @@ int mcpt_render_frames(mcpt_ctx *ctx, const mcpt_scene *scene, const mcpt_camera
   // of frames, then hands the pixel's state to whichever lane takes its next
   // block.  One launch runs many blocks of every pixel, block-major, so lanes
   // stay busy until the last block (no per-block drain of the GPU).
-  // frames_per_launch <= 0: auto — the fewest blocks that give every
-  // resident lane `block_entries` queue entries (so the launch's tail, where
-  // lanes run dry, is at most about 1/block_entries of it), frames split
-  // evenly over them, at most max_block_frames per block.
+  // frames_per_launch <= 0: auto.  Blocks let the launch's tail shrink: the
+  // fewest blocks that give every resident lane `block_entries` queue entries
+  // (so the tail, where lanes run dry, is about 1/block_entries of the
+  // launch), frames split evenly over them, at most max_block_frames each.
+  // That needs several entries per lane in each block (>= 4): a pixel's next
+  // block is then claimed long after its previous one started.  With fewer
+  // (small images, strong-scaled ranks: about one pixel per lane) every block
+  // boundary becomes a wait for the slowest pixel of the previous block, so
+  // blocks there keep at least 4 frames (measured on C2 and C4 shares of 2,
+  // 4 and 8 ranks, tools/sweep.py --stripes).
   const uint32_t n_items = (uint32_t)A.tiles_x * (uint32_t)((A.local_rows + 7) / 8) * 64u;
   int fpl = p->frames_per_launch;
   if (fpl <= 0) {
@@ -1675,7 +1715,8 @@ int mcpt_render_frames(mcpt_ctx *ctx, const mcpt_scene *scene, const mcpt_camera
     int nb = (int)std::ceil(want / std::max(per_block, 1e-9));
     nb = std::max(1, std::min(nb, frames));
     fpl = (frames + nb - 1) / nb;
-    fpl = std::max(1, std::min(fpl, cap));
+    if (per_block < 4.0) fpl = std::max(fpl, 4);
+    fpl = std::max(1, std::min({fpl, cap, frames}));
   }
   // blocks per launch: the hand-off tag holds 12 bits of block index, and
   // one launch covers at most ~4096 frames
@@ -1704,7 +1745,8 @@ int mcpt_render_frames(mcpt_ctx *ctx, const mcpt_scene *scene, const mcpt_camera
   A.fpl = fpl;
   A.handoff = ctx->d_handoff;
   A.spill = ctx->d_spill;
-  if (ctx->stats_on || kDebug) HIP_OK(hipMemsetAsync(ctx->d_stats, 0, kStatSlots * sizeof(unsigned long long), st));
+  if (ctx->stats_on || kDebug || kTiming)
+    HIP_OK(hipMemsetAsync(ctx->d_stats, 0, kStatSlots * sizeof(unsigned long long), st));
   HIP_OK(hipEventRecord(ctx->ev0, st));
   int launches = 0;
   if (tiles > 0 && p->frames > 0) {
@@ -1735,7 +1777,7 @@ int mcpt_render_frames(mcpt_ctx *ctx, const mcpt_scene *scene, const mcpt_camera
   ctx->last.stack_window = win ? 1 : 0;
   ctx->last.workgroups = (int32_t)grid;
   ctx->last_pending = true;
-  ctx->last_stats = ctx->stats_on || kDebug;
+  ctx->last_stats = ctx->stats_on || kDebug || kTiming;
   return MCPT_OK;
 }
 

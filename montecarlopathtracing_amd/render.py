@@ -117,7 +117,9 @@ class Renderer:
     def stats(self):
         s = L.Stats()
         L.check(L.lib().mcpt_get_stats(self.ctx, ctypes.byref(s)))
-        return {f: getattr(s, f) for f, _ in L.Stats._fields_ if f != "pad"}
+        out = {f: getattr(s, f) for f, _ in L.Stats._fields_ if f != "pad"}
+        out["phase_ticks"] = list(out["phase_ticks"])
+        return out
 
     def set_tuning(self, **knobs):
         """mcpt_set_tuning: k_render launch-plan knobs (leaf_threshold,

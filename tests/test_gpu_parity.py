@@ -342,7 +342,8 @@ def _c5_small():
 def test_random_mesh_c5_bitexact(rnd, schedule):
     """C5 (the deep-BVH random mesh): 500 K triangles at 64x64, depth 8, 5
     frames, with the launch plan on auto (the stack layout picked by the
-    occupancy rule, not forced; 5 one-frame blocks handed between lanes).
+    occupancy rule, not forced; the frames split into blocks handed between
+    lanes).
     The reference's own kernels traverse the same tree with their fixed
     int stack[64] (objdef.h:247); images, counts and seeds match bit for
     bit."""
@@ -350,7 +351,7 @@ def test_random_mesh_c5_bitexact(rnd, schedule):
     assert S.bvh_stack_depth(data.nodes) <= 64  # within the reference's stack
     (h_, c_, s_), (rh, rc, rs) = _render_both(rnd, data, S.RANDOM_MESH_CAMERA, 64, 64, 8, 5, 4, schedule=schedule)
     st = rnd.stats()
-    assert st["frames_per_block"] == 1 and st["stack_window"] in (0, 1)
+    assert st["frames_per_block"] < 5 and st["stack_window"] in (0, 1)  # >= 2 blocks: a hand-off happened
     assert_bits_equal(c_, rc, "count")
     assert_bits_equal(s_, rs, "seeds")
     assert_bits_equal(h_, rh, "hist")

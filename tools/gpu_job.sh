@@ -5,6 +5,7 @@
 #   "profile <tag> <args>"   tools/profile.py run (bench line + rocprofv3 passes)
 #   "sweep <args>"           tools/sweep.py        "ab <args>"   tools/ab.py
 #   "bench <args>"           bench.py              "smoke"       __graft_entry__.smoke()
+#   "run <command>"          any other command (600 s limit)
 # Logs: gpurun_out/job_<k>_<kind>.log
 #   gpurun -- bash tools/gpu_job.sh "pytest tests/test_gpu_parity.py" "bench --steps 20 --warmup 5"
 export TMPDIR=/tmp
@@ -22,6 +23,7 @@ for step in "$@"; do
     ab)      cmd="timeout -k 10 900 python -u tools/ab.py $rest" ;;
     bench)   cmd="timeout -k 10 600 python -u bench.py $rest" ;;
     smoke)   cmd="timeout -k 10 300 python -u -c 'import __graft_entry__ as g; g.smoke()'" ;;
+    run)     cmd="timeout -k 10 600 $rest" ;;
     *) echo "unknown step kind: $kind"; exit 2 ;;
   esac
   echo "=== step $k: $step"

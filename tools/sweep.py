@@ -45,6 +45,8 @@ def main():
     ap.add_argument("--schedule", default="paired", choices=["single", "paired"])
     ap.add_argument("--stats", action="store_true")
     ap.add_argument("--json", default=None, help="append result lines to this file")
+    ap.add_argument("--stripes", default="1", help="comma list of stripe counts: rank 0's share of the image "
+                    "(16-row stripes dealt round-robin) rendered alone = one rank of an N-GPU strong-scaled run")
     a = ap.parse_args()
     wl = bench.WORKLOADS[a.workload]
     w, h, depth = wl["w"], wl["h"], wl["depth"]
@@ -54,31 +56,43 @@ def main():
     dsc = rnd.upload(data)
     dsc.schedule = L.SCHED_PAIRED if a.schedule == "paired" else L.SCHED_SINGLE
     st = rnd.new_state(w, h)
-    combos = [(fpl, g) for fpl in (int(x) for x in a.fpl.split(",")) for g in parse_grid(a.grid)]
+    combos = [(fpl, g, n) for n in (int(x) for x in a.stripes.split(",")) for fpl in (int(x) for x in a.fpl.split(","))
+              for g in parse_grid(a.grid)]
     times = {i: [] for i in range(len(combos))}
+    ticks = {}
     fpb = {}
-    for i, (fpl, g) in enumerate(combos):  # warm every variant once
+    for i, (fpl, g, n) in enumerate(combos):  # warm every variant once
         rnd.set_tuning(**g)
-        rnd.render_frames(dsc, cam, st, depth, 1 << 30, min(a.frames, 4), frames_per_launch=fpl)
+        rnd.render_frames(dsc, cam, st, depth, 1 << 30, min(a.frames, 4), frames_per_launch=fpl, stripe_count=n)
     torch.cuda.synchronize()
     for _ in range(a.reps):
-        for i, (fpl, g) in enumerate(combos):
+        for i, (fpl, g, n) in enumerate(combos):
             rnd.set_tuning(**g)
-            rnd.render_frames(dsc, cam, st, depth, 1 << 30, a.frames, frames_per_launch=fpl)
+            rnd.render_frames(dsc, cam, st, depth, 1 << 30, a.frames, frames_per_launch=fpl, stripe_count=n)
             s = rnd.stats()
             times[i].append(s["kernel_ms"])
             fpb[i] = s["frames_per_block"]
+            if any(s["phase_ticks"]):  # an MCPT_PHASE_TIMING build (MCPT_LIB_OVERRIDE)
+                ticks.setdefault(i, [0, 0, 0, 0])
+                ticks[i] = [a + b for a, b in zip(ticks[i], s["phase_ticks"])]
     out = []
-    for i, (fpl, g) in enumerate(combos):
+    for i, (fpl, g, n) in enumerate(combos):
         ts = sorted(times[i])
         med = ts[len(ts) // 2]
         rec = {"workload": a.workload, "frames": a.frames, "fpl": fpl, "fpb": fpb[i], "tuning": g,
                "kernel_ms_median": round(med, 3), "kernel_ms_min": round(ts[0], 3),
                "Msamples_s": round(w * h * a.frames * depth / (med / 1e3) / 1e6, 1)}
+        if i in ticks:
+            tot = float(sum(ticks[i]))
+            rec["phase_frac_fetch_T_L_S"] = [round(t / tot, 4) for t in ticks[i]]
+        if n > 1:  # one rank's share: the N-rank job's rate if every rank took as long
+            rec.update({"stripes": n, "Msamples_s": None,
+                        "rank0_Msamples_s": round(w * h / n * a.frames * depth / (med / 1e3) / 1e6, 1),
+                        "job_Msamples_s_if_balanced": round(w * h * a.frames * depth / (med / 1e3) / 1e6, 1)})
         if a.stats:
             rnd.set_tuning(**g)
             rnd.set_stats(True)
-            rnd.render_frames(dsc, cam, st, depth, 1 << 30, a.frames, frames_per_launch=fpl)
+            rnd.render_frames(dsc, cam, st, depth, 1 << 30, a.frames, frames_per_launch=fpl, stripe_count=n)
             c = rnd.stats()
             rnd.set_stats(False)
             seg = max(c["segments"], 1)
