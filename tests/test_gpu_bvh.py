@@ -3,11 +3,13 @@
 TreeletBVH<CPU> (MCPT/BVH/treeletBVH.cpp, "bvhtype": "treelet") runs on the
 GPU as mcpt_treelet_device; the oracle (oracle/mcpt_oracle_treelet.cpp) is the
 reference's sequential pass written with the same std::push_heap/pop_heap
-calls.  Bar: node arrays bit-identical.  Parity note: the reference host C++
-cannot be compiled here, so the oracle is a restatement; the
-rendered images over the treelet tree are still checked bit for bit against
-the reference's own kernels (test_gpu_parity.py).
+calls.  Bar: node arrays bit-identical.  The oracle is itself pinned by the
+reference's own TreeletBVH<CPU>, compiled unmodified (oracle/ref_host_golden,
+tests/golden/ref_host.npz), and the GPU pass is compared with those fixtures
+directly below.
 """
+import os
+
 import numpy as np
 import pytest
 
@@ -16,6 +18,7 @@ torch = pytest.importorskip("torch")
 pytestmark = pytest.mark.gpu
 
 from montecarlopathtracing_amd import _lib as L  # noqa: E402
+from montecarlopathtracing_amd import bvhtest as B  # noqa: E402
 from montecarlopathtracing_amd import render as R  # noqa: E402
 from montecarlopathtracing_amd import scene as S  # noqa: E402
 
@@ -119,8 +122,6 @@ def test_app_unknown_bvhtype_raises():
 
 
 # ------------------------------------------------------ testbvh metrics
-from montecarlopathtracing_amd import bvhtest as B  # noqa: E402
-
 from . import refgpu  # noqa: E402
 
 needs_ref = pytest.mark.skipif(not refgpu.available(), reason="oracle/_ref not built")
@@ -198,3 +199,30 @@ def test_cli_testbvh_and_testall():
         assert r.returncode == 0, r.stderr
         for w in want:
             assert w in r.stdout, r.stdout
+
+
+# ------------------------------------------- the reference's own host C++
+def _sha(a):
+    import hashlib
+    return hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()
+
+
+@pytest.mark.parametrize("name", ["cbox", "mis", "random20k"])
+def test_gpu_treelet_equals_reference_host(name):
+    """mcpt_treelet_device == TreeletBVH<CPU> (BVH/treeletBVH.cpp:30-372)
+    compiled unmodified from the reference (tests/golden/ref_host.npz,
+    tools/make_host_goldens.py), byte for byte."""
+    g = np.load(os.path.join(scenes.ROOT, "tests", "golden", "ref_host.npz"))
+    nodes = {"cbox": lambda: scenes.cbox().nodes, "mis": lambda: scenes.mis().nodes,
+             "random20k": lambda: S.random_mesh(20_000, seed=11).nodes}[name]()
+    assert _sha(nodes) == str(g["treelet_%s_in_sha" % name])
+    assert _sha(R.treelet_device(nodes)) == str(g["treelet_%s_out_sha" % name])
+
+
+def test_gpu_lcv_equals_reference_host():
+    """mcpt_bvh_lcv_device == BVH::TEST::LCV (bvhtest.cpp:324-444) compiled
+    from the reference (cbox, config 2's 256 x 256), float bits."""
+    g = np.load(os.path.join(scenes.ROOT, "tests", "golden", "ref_host.npz"))
+    w, h = (int(x) for x in g["lcv_size"])
+    v = B.lcv(scenes.cbox().nodes, S.parse_camera(scenes.CBOX_CAM), w, h)
+    assert np.float32(v).view(np.uint32) == g["lcv_cbox_bits"]
