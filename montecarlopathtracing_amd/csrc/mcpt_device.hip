@@ -36,7 +36,7 @@
 using namespace mcpt;
 
 #ifndef MCPT_WAVES_PER_SIMD
-#define MCPT_WAVES_PER_SIMD 4  // k_render occupancy target (tools/sweep_waves.sh)
+#define MCPT_WAVES_PER_SIMD 4  // k_render occupancy target (tools/sweep.py over `make variants`)
 #endif
 #ifndef MCPT_STACK_WINDOW_K
 #define MCPT_STACK_WINDOW_K 32
@@ -1633,7 +1633,7 @@ int mcpt_render_frames(mcpt_ctx *ctx, const mcpt_scene *scene, const mcpt_camera
   A.max_depth = p->max_depth;
   A.max_attempt = p->max_attempt;
   A.stack_depth = scene->stack_depth;
-  // tuned (tools/sweep_env.sh, tools/gpu_thr.sh): leaf phase at >= 4 lanes
+  // tuned (tools/sweep.py, tools/ab.py): leaf phase at >= 4 lanes
   // (single-leaf schedule) or >= 16 (paired), shade at >= 32
   const mcpt_tuning &T = ctx->tune;
   const bool pair = p->schedule == MCPT_SCHED_PAIRED;

@@ -1,5 +1,8 @@
 """One rank of tests/test_gpu_dist.py: dist.render_distributed over a gloo
-group whose ranks share the box's one GPU; rank 0 saves the reduced image."""
+group whose ranks share the box's one GPU, or over RCCL ("nccl") with one rank
+(RCCL refuses two ranks on one device); rank 0 saves the reduced image.
+
+    _dist_render_worker.py <out.npz> [gloo|nccl]"""
 import os
 import sys
 
@@ -18,9 +21,9 @@ from tests import scenes  # noqa: E402
 W, H, DEPTH, FRAMES = 160, 120, 6, 4
 
 
-def main(out):
+def main(out, backend):
     torch.cuda.set_device(0)
-    dist.init_process_group("gloo")
+    dist.init_process_group(backend)
     rnd = R.Renderer(0)
     sc = rnd.upload(scenes.cbox())
     res = D.render_distributed(rnd, sc, S.parse_camera(scenes.CBOX_CAM), W, H, DEPTH, 1 << 20, FRAMES,
@@ -33,4 +36,4 @@ def main(out):
 
 
 if __name__ == "__main__":
-    main(sys.argv[1])
+    main(sys.argv[1], sys.argv[2] if len(sys.argv) > 2 else "gloo")

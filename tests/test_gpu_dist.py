@@ -1,8 +1,9 @@
 """dist.render_distributed end to end: N ranks render their
 row stripes and one reduce sums them onto rank 0; the image must be
 bit-identical to one GPU rendering the whole frame.  Rehearsed with ranks
-sharing the box's one GPU over gloo (the RCCL run is the same code with
-backend "nccl")."""
+sharing the box's one GPU over gloo, and over RCCL (backend "nccl") with one
+rank, since RCCL refuses two ranks on one device: that run takes the
+device-tensor reduce path the 8-GPU job uses."""
 import os
 import socket
 import subprocess
@@ -24,8 +25,8 @@ def _port():
     return p
 
 
-@pytest.mark.parametrize("ranks", [2, 3])
-def test_render_distributed_equals_one_gpu(tmp_path, ranks):
+@pytest.mark.parametrize("ranks,backend", [(2, "gloo"), (3, "gloo"), (1, "nccl")])
+def test_render_distributed_equals_one_gpu(tmp_path, ranks, backend):
     from montecarlopathtracing_amd import render as R
     from montecarlopathtracing_amd import scene as S
     from tests import _dist_render_worker as Wk
@@ -33,7 +34,7 @@ def test_render_distributed_equals_one_gpu(tmp_path, ranks):
     out = str(tmp_path / "img.npz")
     r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(ranks),
                         "--master-addr", "127.0.0.1", "--master-port", str(_port()),
-                        os.path.join(ROOT, "tests", "_dist_render_worker.py"), out],
+                        os.path.join(ROOT, "tests", "_dist_render_worker.py"), out, backend],
                        cwd=ROOT, capture_output=True, text=True, timeout=240)
     assert r.returncode == 0, r.stderr[-3000:]
     got = np.load(out)
