@@ -35,6 +35,9 @@
 
 using namespace mcpt;
 
+#ifndef MCPT_PROBE
+#define MCPT_PROBE 0  // sensitivity probes of `make variants` (p1: +1 gather, p2: +16 VALU per node step)
+#endif
 #ifndef MCPT_WAVES_PER_SIMD
 #define MCPT_WAVES_PER_SIMD 4  // k_render occupancy target (tools/sweep.py over `make variants`)
 #endif
@@ -867,7 +870,24 @@ __global__ void __launch_bounds__(64, MCPT_WAVES_PER_SIMD) k_render(RenderArgs A
           uint32_t ctr = 0;
           const DevNode4 *__restrict__ tree = ref ? S.nodes4 : S.near4;
           if (MCPT_DCHECK(cur < (ref ? S.n_nodes4 : S.n_near4), 1)) {
+#if MCPT_PROBE == 1  // sensitivity probe (not shipped): one more 16-B gather per node step
+            const f4 pad = tree[cur].pad;
+#elif MCPT_PROBE == 3  // one more 4-B gather per node step (same line)
+            const f4 pad = (f4){reinterpret_cast<const float *>(&tree[cur].pad)[0], 0.0f, 0.0f, 0.0f};
+#elif MCPT_PROBE == 4  // one more 16-B load per node step, the same address in every lane
+            const f4 pad = tree[0].pad;
+#endif
             cur = step4<PRUNE>(tree[cur], o.xyz, rinv, kTmin, best_t + S.prune_margin, !ref, stk, sp, ctr);
+#if MCPT_PROBE == 1 || MCPT_PROBE == 3 || MCPT_PROBE == 4
+            if (__builtin_expect(as_i(pad.x) == 0x7FC0DEAD, 0)) cur = kPop;
+#elif MCPT_PROBE == 2  // sensitivity probe (not shipped): 16 more VALU per node step
+            {
+              float x = rinv.x;
+#pragma unroll
+              for (int k = 0; k < 16; ++k) x = fmaf(x, 1.0001f, rinv.y);
+              if (__builtin_expect(as_i(x) == 0x7FC0DEAD, 0)) cur = kPop;
+            }
+#endif
             if (!MCPT_DCHECK(sp <= stack_cap, 0)) sp = stack_cap;
           } else {
             cur = kPop;
