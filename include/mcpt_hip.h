@@ -164,6 +164,11 @@ typedef struct mcpt_stats {
   uint64_t phase_ticks[4];          /* MCPT_PHASE_TIMING builds: shader-clock ticks
                                        all waves spent in fetch, T, L, S (0 in
                                        release builds)                        */
+  uint64_t leaf_rejects;            /* stats on, quantized tree: leaves the search
+                                       reached whose exact box the ray misses */
+  int32_t  quantized;               /* 1: the last call searched the 64-B
+                                       quantized tree (EXACT mode)            */
+  int32_t  pad1;
 } mcpt_stats;
 
 /* Launch-plan knobs of the fused kernel (speed only: every setting gives the
@@ -184,6 +189,10 @@ typedef struct mcpt_tuning {
   int32_t lds_pad;          /* extra LDS bytes per workgroup (occupancy
                                experiments; 0)                                    */
   int32_t queues;           /* work queues (1..8; 8: one per XCD)              */
+  int32_t quantized;        /* EXACT search tree: 0 auto (the 64-B quantized
+                               nodes when the 128-B tree exceeds 32 MiB, the
+                               GPU's aggregate L2), 1 quantized whenever the
+                               scene has them, 2 the 128-B nodes                 */
 } mcpt_tuning;
 
 /* ------------------------------------------------------- version / errors */

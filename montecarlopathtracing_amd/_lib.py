@@ -48,14 +48,15 @@ class Stats(ctypes.Structure):
                 ("wave_shade_phases", ctypes.c_uint64), ("order_fallbacks", ctypes.c_uint64),
                 ("wave_iterations", ctypes.c_uint64), ("lane_waiting", ctypes.c_uint64), ("lane_idle", ctypes.c_uint64),
                 ("stack_window", ctypes.c_int32), ("workgroups", ctypes.c_int32),
-                ("debug_violations", ctypes.c_uint64), ("phase_ticks", ctypes.c_uint64 * 4)]
+                ("debug_violations", ctypes.c_uint64), ("phase_ticks", ctypes.c_uint64 * 4),
+                ("leaf_rejects", ctypes.c_uint64), ("quantized", ctypes.c_int32), ("pad1", ctypes.c_int32)]
 
 
 class Tuning(ctypes.Structure):
     """mcpt_tuning: launch-plan knobs of k_render (speed only; 0 = default)."""
     _fields_ = [(n, ctypes.c_int32) for n in (
         "leaf_threshold", "shade_threshold", "queue_chunk", "block_entries", "max_block_frames", "stack_window",
-        "lds_pad", "queues")]
+        "lds_pad", "queues", "quantized")]
 
 
 class MCPTError(RuntimeError):

@@ -84,6 +84,25 @@ struct __attribute__((aligned(16))) DevNode4 {
   f4 pad;
 };
 static_assert(sizeof(DevNode4) == 128 && sizeof(DevNode4) == sizeof(mcpt::Node4Rec), "128-B 4-wide node");
+// 64-B quantized search-tree node (mcpt::Node4Q): four 16-B loads.  c0 =
+// (origin.xyz, scale.x); qb[0..5] = the 24 plane bytes in DevNode4::q order
+// (decoded fma(q, s, o): a strictly larger box than the exact one); then
+// scale.y, scale.z and the four links.
+struct __attribute__((aligned(16))) DevNode4Q {
+  f4 c0;
+  uint32_t qb[6];
+  float sy, sz;
+  int32_t link[4];
+};
+static_assert(sizeof(DevNode4Q) == 64 && sizeof(DevNode4Q) == sizeof(mcpt::Node4Q), "64-B quantized node");
+// Triangle record of the quantized path: the raw vertices (so the L phase can
+// rebuild the reference leaf's exact box, hlbvh.cpp:97-100) with the three
+// triangle-only Cramer minors in .w, then the packed normal / material id.
+struct __attribute__((aligned(16))) DevTriQ {
+  f4 v0, v1, v2, nrm;
+};
+static_assert(sizeof(DevTriQ) == 64, "64-B triangle");
+
 constexpr int32_t kDone = INT32_MIN;           // traversal finished
 constexpr int32_t kPop = INT32_MIN + 1;        // take the next entry from the stack
 constexpr int32_t kEmptySlot = INT32_MIN + 2;  // unused 4-wide slot
@@ -96,6 +115,8 @@ struct SceneView {
   const DevNode4 *nodes4;  // the reference HLBVH collapsed 4-wide (left-first fallback)
   const DevNode *nodes;
   const DevTri *tris;
+  const DevNode4Q *near4q;  // near4 quantized (nullptr: the scene keeps the 128-B nodes only)
+  const DevTriQ *triq;      // triangles for the quantized path
   const mcpt_material *mats;
   f4 root_min, root_max;
   int32_t root_leaf;  // >= 0: single-triangle scene, root is that leaf
@@ -110,6 +131,9 @@ struct mcpt_scene {
   int32_t stack_depth4 = 1;  // EXACT: max of both 4-wide trees' stack needs
   DevNode *nodes = nullptr;
   DevTri *tris = nullptr;
+  DevNode4Q *near4q = nullptr;
+  DevTriQ *triq = nullptr;
+  int64_t near4_bytes = 0;  // the 128-B search tree's size (auto choice of the quantized one)
   mcpt_material *mats = nullptr;
   int64_t n_tris = 0, n_internal = 0;
   int32_t n_mats = 0;
@@ -120,7 +144,8 @@ struct mcpt_scene {
 constexpr int kQueues = 8;         // k_render work queues (at most): one per XCD (MI355X has 8)
 constexpr int kQueueStride = 32;   // u32 words between queue heads: one 128-B line each
 constexpr int kHandoffWords = 6;   // seed, mean.xyzw, count: one tagged 8-B granule each
-constexpr int kStatSlots = 24;     // k_render counters (mcpt_stats)
+constexpr int kStatSlots = 24;
+constexpr int64_t kQuantAutoBytes = 32ll << 20;  // 8 XCDs x 4 MiB of L2     // k_render counters (mcpt_stats)
 constexpr int kPhaseSlot = 16;     // MCPT_PHASE_TIMING: shader-clock ticks per phase (fetch, T, L, S)
 constexpr int kDebugSlot = 12;     // MCPT_DEBUG: violations of the stack bound, node and triangle indices
 
@@ -677,10 +702,11 @@ __device__ inline uint32_t queue_items(uint32_t x, uint32_t n_tiles, uint32_t nq
 // run).  Expensive phases therefore execute with most of the wave active
 // instead of once per diverging lane.  Each lane's own
 // sequence of operations is exactly the reference's, so results are unchanged.
-template <int MODE, bool STATS, bool WIN, bool PAIR>
+template <int MODE, bool STATS, bool WIN, bool PAIR, bool Q>
 __global__ void __launch_bounds__(64, MCPT_WAVES_PER_SIMD) k_render(RenderArgs A) {
   constexpr bool PRUNE = MODE != MCPT_MODE_NOPRUNE;
   constexpr bool LIT = MODE == MCPT_MODE_NOPRUNE;
+  static_assert(!(Q && LIT), "the quantized search tree is an EXACT-mode structure");
   extern __shared__ int32_t lds_stack[];
   const int lane = threadIdx.x;
   // the whole stack in LDS, or its top kStackWindow entries (deep trees, where
@@ -705,7 +731,7 @@ __global__ void __launch_bounds__(64, MCPT_WAVES_PER_SIMD) k_render(RenderArgs A
 
   unsigned long long n_seg = 0, n_nodes = 0, n_tests = 0, n_bad = 0;
   unsigned long long w_t = 0, w_l = 0, w_s = 0, n_fb = 0;
-  unsigned long long w_it = 0, n_wait = 0, n_idle = 0;
+  unsigned long long w_it = 0, n_wait = 0, n_idle = 0, n_rej = 0;
   // pixel state.  lst: this lane's role in the queue protocol, one small
   // int (one VGPR; kept out of lane-mask SGPR pairs on purpose, SGPRs are
   // the scarce register file of this kernel)
@@ -733,6 +759,7 @@ __global__ void __launch_bounds__(64, MCPT_WAVES_PER_SIMD) k_render(RenderArgs A
   // traverse_exact); t2 = runner-up t of the nearest-first search
   bool ref = LIT;
   float t2 = kFltMax;
+  auto pop_next = [&]() -> int32_t { return sp == 0 ? kDone : stk.pop(sp); };
   auto begin_segment = [&]() {
     rinv.x = __builtin_amdgcn_rcpf(d.x);
     rinv.y = __builtin_amdgcn_rcpf(d.y);
@@ -866,7 +893,40 @@ __global__ void __launch_bounds__(64, MCPT_WAVES_PER_SIMD) k_render(RenderArgs A
     if (__ballot(in_t)) {
       if (STATS && lane == __builtin_ctzll(__ballot(1))) w_t++;
       if (in_t) {
-        if (!LIT) {  // EXACT: SAH tree nearest-first, or the reference tree left-first
+        if (Q) {  // EXACT, quantized SAH tree nearest-first (4 loads), or the reference tree left-first
+          uint32_t ctr = 0;
+          if (MCPT_DCHECK(cur < (ref ? S.n_nodes4 : S.n_near4), 1)) {
+            f4 q0, q1, q2, q3, q4, q5;
+            int32_t l0, l1, l2, l3;
+            if (!ref) {
+              const f4 *p = reinterpret_cast<const f4 *>(S.near4q + cur);
+              const f4 c0 = p[0], c1 = p[1], c2 = p[2], c3 = p[3];
+              const float ox = c0.x, oy = c0.y, oz = c0.z, sx = c0.w, sy = c2.z, sz = c2.w;
+              // plane byte k of a word, decoded as fma(q, s, o) (v_cvt_f32_ubyte + fma)
+              auto dec = [](uint32_t w, float sa, float oa, float sb, float ob) -> f4 {
+                return (f4){__builtin_fmaf((float)(w & 0xFFu), sa, oa), __builtin_fmaf((float)((w >> 8) & 0xFFu), sa, oa),
+                            __builtin_fmaf((float)((w >> 16) & 0xFFu), sb, ob), __builtin_fmaf((float)(w >> 24), sb, ob)};
+              };
+              q0 = dec(as_u(c1.x), sx, ox, sy, oy);  // slot 0: x x y y
+              q1 = dec(as_u(c1.y), sz, oz, sx, ox);  // slot 0: z z | slot 1: x x
+              q2 = dec(as_u(c1.z), sy, oy, sz, oz);  // slot 1: y y z z
+              q3 = dec(as_u(c1.w), sx, ox, sy, oy);  // slot 2: x x y y
+              q4 = dec(as_u(c2.x), sz, oz, sx, ox);  // slot 2: z z | slot 3: x x
+              q5 = dec(as_u(c2.y), sy, oy, sz, oz);  // slot 3: y y z z
+              l0 = as_i(c3.x), l1 = as_i(c3.y), l2 = as_i(c3.z), l3 = as_i(c3.w);
+            } else {
+              const DevNode4 &N = S.nodes4[cur];
+              q0 = N.q[0], q1 = N.q[1], q2 = N.q[2], q3 = N.q[3], q4 = N.q[4], q5 = N.q[5];
+              l0 = N.link[0], l1 = N.link[1], l2 = N.link[2], l3 = N.link[3];
+            }
+            cur = step4q<PRUNE>(q0, q1, q2, q3, q4, q5, l0, l1, l2, l3, o.xyz, rinv, kTmin, best_t + S.prune_margin,
+                                !ref, stk, sp, ctr);
+            if (!MCPT_DCHECK(sp <= stack_cap, 0)) sp = stack_cap;
+          } else {
+            cur = kPop;
+          }
+          if (STATS) n_nodes += ctr;
+        } else if (!LIT) {  // EXACT: SAH tree nearest-first, or the reference tree left-first
           uint32_t ctr = 0;
           const DevNode4 *__restrict__ tree = ref ? S.nodes4 : S.near4;
           if (MCPT_DCHECK(cur < (ref ? S.n_nodes4 : S.n_near4), 1)) {
@@ -908,7 +968,7 @@ __global__ void __launch_bounds__(64, MCPT_WAVES_PER_SIMD) k_render(RenderArgs A
           cur = hl ? N.left : (hr ? N.right : kPop);
           if (!MCPT_DCHECK(sp <= stack_cap, 0)) sp = stack_cap;
         }
-        if (cur == kPop) cur = sp == 0 ? kDone : stk.pop(sp);
+        if (cur == kPop) cur = pop_next();
       }
     }
     MCPT_TICK(1);
@@ -923,13 +983,36 @@ __global__ void __launch_bounds__(64, MCPT_WAVES_PER_SIMD) k_render(RenderArgs A
         // the lane's sequence of tests is unchanged, one phase serves two leaves
         const int32_t nx = !PAIR || sp == 0 ? kDone : stk.peek(sp);
         const bool two = PAIR && nx < 0 && nx != kDone;
-        const DevTri T = S.tris[MCPT_DCHECK(~cur < S.n_tris, 2) ? ~cur : 0];
-        DevTri T2;
-        if (two) T2 = S.tris[MCPT_DCHECK(~nx < S.n_tris, 2) ? ~nx : 0];
-        auto test = [&](const DevTri &X) {
-          TriHit h = LIT ? cramer(d.xyz, X.nab.xyz, X.nac.xyz, X.v0.xyz - o.xyz, X.nrm.xyz, kTmin)
-                         : cramer_reduced(d.xyz, X.nab.xyz, X.nac.xyz, X.v0.xyz - o.xyz, X.nrm.xyz, X.v0.w,
-                                          X.nab.w, X.nac.w, kTmin);
+        using Tri = typename std::conditional<Q, DevTriQ, DevTri>::type;
+        const Tri *tri_arr;
+        if constexpr (Q)
+          tri_arr = S.triq;
+        else
+          tri_arr = S.tris;
+        const Tri T = tri_arr[MCPT_DCHECK(~cur < S.n_tris, 2) ? ~cur : 0];
+        Tri T2;
+        if (two) T2 = tri_arr[MCPT_DCHECK(~nx < S.n_tris, 2) ? ~nx : 0];
+        auto test = [&](const Tri &X) {
+          TriHit h;
+          if constexpr (Q) {
+            // the reference leaf's own box (hlbvh.cpp:97-100: min/max of the
+            // vertices; equal to the stored box, checked at upload), tested with
+            // the reference's arithmetic: the search tree's quantized boxes only
+            // ever let MORE leaves through, this restores exactly its set
+            const f2 bx = (f2){fminf(fminf(X.v0.x, X.v1.x), X.v2.x), fmaxf(fmaxf(X.v0.x, X.v1.x), X.v2.x)};
+            const f2 by = (f2){fminf(fminf(X.v0.y, X.v1.y), X.v2.y), fmaxf(fmaxf(X.v0.y, X.v1.y), X.v2.y)};
+            const f2 bz = (f2){fminf(fminf(X.v0.z, X.v1.z), X.v2.z), fmaxf(fmaxf(X.v0.z, X.v1.z), X.v2.z)};
+            const bool leaf = slab_pass(slab_pairs(bx, by, bz, o.xyz, rinv), kTmin);
+            // objdef.h:190-199: AB = v1 - v0, AC = v2 - v0, matrix rows -AB, -AC
+            const f3 nab = -(X.v1.xyz - X.v0.xyz), nac = -(X.v2.xyz - X.v0.xyz);
+            h = cramer_reduced(d.xyz, nab, nac, X.v0.xyz - o.xyz, X.nrm.xyz, X.v0.w, X.v1.w, X.v2.w, kTmin);
+            h.accept = h.accept && leaf;
+            if (STATS) n_rej += !leaf;
+          } else {
+            h = LIT ? cramer(d.xyz, X.nab.xyz, X.nac.xyz, X.v0.xyz - o.xyz, X.nrm.xyz, kTmin)
+                    : cramer_reduced(d.xyz, X.nab.xyz, X.nac.xyz, X.v0.xyz - o.xyz, X.nrm.xyz, X.v0.w, X.nab.w,
+                                     X.nac.w, kTmin);
+          }
           if (STATS) n_tests++;
           if (h.accept) {
             if (ref ? best_t - h.t >= kEps : h.t < best_t) best_nrm = X.nrm;  // objdef.h:213
@@ -945,7 +1028,7 @@ __global__ void __launch_bounds__(64, MCPT_WAVES_PER_SIMD) k_render(RenderArgs A
           (void)stk.pop(sp);
           test(T2);
         }
-        cur = sp == 0 ? kDone : stk.pop(sp);
+        cur = pop_next();
       }
     }
     MCPT_TICK(2);
@@ -1031,6 +1114,7 @@ __global__ void __launch_bounds__(64, MCPT_WAVES_PER_SIMD) k_render(RenderArgs A
     if (w_it) atomicAdd(&A.stats[8], w_it);
     if (n_wait) atomicAdd(&A.stats[9], n_wait);
     if (n_idle) atomicAdd(&A.stats[10], n_idle);
+    if (n_rej) atomicAdd(&A.stats[11], n_rej);
   }
 }
 
@@ -1324,6 +1408,7 @@ int mcpt_get_stats(mcpt_ctx *c, mcpt_stats *out) {
       c->last.wave_iterations = h[8];
       c->last.lane_waiting = h[9];
       c->last.lane_idle = h[10];
+      c->last.leaf_rejects = h[11];
       c->last.debug_violations = h[kDebugSlot] + h[kDebugSlot + 1] + h[kDebugSlot + 2];
       for (int k = 0; k < 4; ++k) c->last.phase_ticks[k] = h[kPhaseSlot + k];
     }
@@ -1334,7 +1419,7 @@ int mcpt_get_stats(mcpt_ctx *c, mcpt_stats *out) {
 
 int mcpt_set_tuning(mcpt_ctx *c, const mcpt_tuning *t) {
   if (!c) return mcpt::fail(MCPT_ERR_ARG, "set_tuning: null ctx");
-  if (t && (t->stack_window < 0 || t->stack_window > 2 || t->lds_pad < 0 || t->lds_pad > 65536 ||
+  if (t && (t->stack_window < 0 || t->stack_window > 2 || t->quantized < 0 || t->quantized > 2 || t->lds_pad < 0 || t->lds_pad > 65536 ||
             t->queue_chunk > 4096 || t->leaf_threshold > 64 || t->shade_threshold > 64))
     return mcpt::fail(MCPT_ERR_ARG, "set_tuning: value out of range");
   if (t)
@@ -1538,6 +1623,42 @@ int mcpt_scene_upload(mcpt_ctx *ctx, const mcpt_triangle *tris, int64_t n_tris, 
     d.nac = (f4){c1, c2, c3, std::fma(b1, c2, -(c1 * b2))};
     d.nrm = (f4){t.normal[0], t.normal[1], t.normal[2], t.normal[3]};
   }
+  // The quantized search tree: 64-B nodes whose decoded
+  // boxes strictly contain the exact ones, so every box test is a superset of
+  // the exact one, and the L phase re-tests the reference leaf's own box,
+  // rebuilt from the triangle's vertices -- valid when every reference leaf's
+  // box IS min/max of its vertices (hlbvh.cpp:97-100; a foreign tree may differ,
+  // and then keeps the 128-B path).
+  std::vector<DevNode4Q> nq;
+  std::vector<DevTriQ> tq;
+  bool quant = n_int > 0;
+  for (int64_t i = 0; quant && i < n_nodes; ++i) {
+    const mcpt_bvh_node &b = nodes[i];
+    if (b.left != b.right) continue;
+    const mcpt_triangle &t = tris[b.left];
+    for (int a = 0; a < 3; ++a) {
+      const float lo = std::min(std::min(t.v[0][a], t.v[1][a]), t.v[2][a]);
+      const float hi = std::max(std::max(t.v[0][a], t.v[1][a]), t.v[2][a]);
+      if (!(b.bbmin[a] == lo && b.bbmax[a] == hi)) quant = false;
+    }
+  }
+  if (quant) {
+    nq.resize(near.size());
+    for (size_t k = 0; quant && k < near.size(); ++k)
+      quant = mcpt::quantize_node4(near[k], *reinterpret_cast<mcpt::Node4Q *>(&nq[k])) == 0;
+  }
+  if (quant) {
+    tq.resize(n);
+    for (int64_t i = 0; i < n; ++i) {
+      const mcpt_triangle &t = tris[i];
+      tq[i].v0 = (f4){t.v[0][0], t.v[0][1], t.v[0][2], dt[i].v0.w};
+      tq[i].v1 = (f4){t.v[1][0], t.v[1][1], t.v[1][2], dt[i].nab.w};
+      tq[i].v2 = (f4){t.v[2][0], t.v[2][1], t.v[2][2], dt[i].nac.w};
+      tq[i].nrm = dt[i].nrm;
+    }
+  } else {
+    nq.clear();
+  }
   // pruning margin: 2^-10 of the scene diagonal
   const mcpt_bvh_node &root = nodes[0];
   float dx = root.bbmax[0] - root.bbmin[0], dy = root.bbmax[1] - root.bbmin[1], dz = root.bbmax[2] - root.bbmin[2];
@@ -1562,7 +1683,15 @@ int mcpt_scene_upload(mcpt_ctx *ctx, const mcpt_triangle *tris, int64_t n_tris, 
     mcpt_scene_destroy(s);
     return mcpt::fail(MCPT_ERR_HIP, "scene_upload: hipMemcpy failed");
   }
+  if (quant && (hipMalloc(&s->near4q, nq.size() * sizeof(DevNode4Q)) != hipSuccess ||
+                hipMalloc(&s->triq, tq.size() * sizeof(DevTriQ)) != hipSuccess ||
+                hipMemcpy(s->near4q, nq.data(), nq.size() * sizeof(DevNode4Q), hipMemcpyHostToDevice) != hipSuccess ||
+                hipMemcpy(s->triq, tq.data(), tq.size() * sizeof(DevTriQ), hipMemcpyHostToDevice) != hipSuccess)) {
+    mcpt_scene_destroy(s);
+    return mcpt::fail(MCPT_ERR_HIP, "scene_upload: quantized tree upload failed");
+  }
   s->n_tris = n;
+  s->near4_bytes = (int64_t)(near.size() * sizeof(DevNode4));
   s->n_internal = n_int;
   s->n_mats = n_mats;
   s->stack_depth = std::max(depth, 1);
@@ -1576,6 +1705,8 @@ int mcpt_scene_upload(mcpt_ctx *ctx, const mcpt_triangle *tris, int64_t n_tris, 
   v.nodes4 = s->nodes4;
   v.near4 = s->near4;
   v.tris = s->tris;
+  v.near4q = s->near4q;
+  v.triq = s->triq;
   v.mats = s->mats;
   v.root_min = (f4){root.bbmin[0], root.bbmin[1], root.bbmin[2], root.bbmin[3]};
   v.root_max = (f4){root.bbmax[0], root.bbmax[1], root.bbmax[2], root.bbmax[3]};
@@ -1593,6 +1724,8 @@ int mcpt_scene_destroy(mcpt_scene *s) {
   if (s->nodes4) (void)hipFree(s->nodes4);
   if (s->near4) (void)hipFree(s->near4);
   if (s->tris) (void)hipFree(s->tris);
+  if (s->near4q) (void)hipFree(s->near4q);
+  if (s->triq) (void)hipFree(s->triq);
   if (s->mats) (void)hipFree(s->mats);
   delete s;
   return MCPT_OK;
@@ -1669,14 +1802,21 @@ int mcpt_render_frames(mcpt_ctx *ctx, const mcpt_scene *scene, const mcpt_camera
   // The stack lives in LDS; when the whole stack would allow fewer resident
   // workgroups than a kStackWindow window does, the windowed kernel runs.
   const bool noprune = p->mode == MCPT_MODE_NOPRUNE;
-  // [noprune][stats][window][pair]
-#define MCPT_KR(M, ST, W) {(const void *)k_render<M, ST, W, false>, (const void *)k_render<M, ST, W, true>}
-  static const void *const kfns[2][2][2][2] = {
-      {{MCPT_KR(MCPT_MODE_EXACT, false, false), MCPT_KR(MCPT_MODE_EXACT, false, true)},
-       {MCPT_KR(MCPT_MODE_EXACT, true, false), MCPT_KR(MCPT_MODE_EXACT, true, true)}},
-      {{MCPT_KR(MCPT_MODE_NOPRUNE, false, false), MCPT_KR(MCPT_MODE_NOPRUNE, false, true)},
-       {MCPT_KR(MCPT_MODE_NOPRUNE, true, false), MCPT_KR(MCPT_MODE_NOPRUNE, true, true)}}};
+  // [kind: 0 EXACT 128-B nodes, 1 NOPRUNE, 2 EXACT quantized][stats][window][pair]
+#define MCPT_KR(M, ST, W, QN) {(const void *)k_render<M, ST, W, false, QN>, (const void *)k_render<M, ST, W, true, QN>}
+#define MCPT_KK(M, QN) {{MCPT_KR(M, false, false, QN), MCPT_KR(M, false, true, QN)}, \
+                        {MCPT_KR(M, true, false, QN), MCPT_KR(M, true, true, QN)}}
+  static const void *const kfns[3][2][2][2] = {MCPT_KK(MCPT_MODE_EXACT, false), MCPT_KK(MCPT_MODE_NOPRUNE, false),
+                                               MCPT_KK(MCPT_MODE_EXACT, true)};
+#undef MCPT_KK
 #undef MCPT_KR
+  // quantized search tree: forced on (1) or off (2), or auto (0): on when the
+  // 128-B tree outgrows the GPU's aggregate L2, where its halved node bytes and
+  // gathers pay (C5 -6 %); on cache-resident trees its looser boxes cost more
+  // node steps and leaf tests than the saved gathers (C2 +6 %, C3 +11 %;
+  // profiles/r02_quant_ab.txt)
+  const bool quant = scene->near4q && (T.quantized == 1 || (T.quantized == 0 && scene->near4_bytes > kQuantAutoBytes));
+  const int kind = noprune ? 1 : (quant ? 2 : 0);
   const size_t pad = (size_t)std::max(0, T.lds_pad);
   const size_t lds_plain = (size_t)depth_entries * 64 * sizeof(int32_t) + lds_mats + pad;
   const size_t lds_win = (size_t)kStackWindow * 64 * sizeof(int32_t) + lds_mats + pad;
@@ -1684,22 +1824,22 @@ int mcpt_render_frames(mcpt_ctx *ctx, const mcpt_scene *scene, const mcpt_camera
   int per_cu = 0;
   if (T.stack_window == 1) {  // forced (tests, experiments): the window even when the whole stack fits in it
     win = true;
-    rc = occupancy(ctx, kfns[noprune][ctx->stats_on][1][pair], lds_win, &per_cu);
+    rc = occupancy(ctx, kfns[kind][ctx->stats_on][1][pair], lds_win, &per_cu);
     if (rc) return rc;
   } else if (depth_entries > kStackWindow && T.stack_window != 2) {
     int per_cu_plain = 0, per_cu_win = 0;
-    rc = occupancy(ctx, kfns[noprune][ctx->stats_on][0][pair], lds_plain, &per_cu_plain);
+    rc = occupancy(ctx, kfns[kind][ctx->stats_on][0][pair], lds_plain, &per_cu_plain);
     if (rc) return rc;
-    rc = occupancy(ctx, kfns[noprune][ctx->stats_on][1][pair], lds_win, &per_cu_win);
+    rc = occupancy(ctx, kfns[kind][ctx->stats_on][1][pair], lds_win, &per_cu_win);
     if (rc) return rc;
     win = T.stack_window == 1 || per_cu_win > per_cu_plain;
     per_cu = win ? per_cu_win : per_cu_plain;
   } else {
-    rc = occupancy(ctx, kfns[noprune][ctx->stats_on][0][pair], lds_plain, &per_cu);
+    rc = occupancy(ctx, kfns[kind][ctx->stats_on][0][pair], lds_plain, &per_cu);
     if (rc) return rc;
   }
   const size_t lds = win ? lds_win : lds_plain;
-  const void *kfn = kfns[noprune][ctx->stats_on][win][pair];
+  const void *kfn = kfns[kind][ctx->stats_on][win][pair];
   A.stack_depth = win ? kStackWindow : depth_entries;  // the material table follows the stack in LDS
   A.spill_stride = win ? std::max(0, depth_entries - kStackWindow) : 0;
   const int64_t grid = std::max<int64_t>(1, std::min<int64_t>(tiles, (int64_t)std::max(per_cu, 1) * ctx->n_cu));
@@ -1795,6 +1935,7 @@ int mcpt_render_frames(mcpt_ctx *ctx, const mcpt_scene *scene, const mcpt_camera
   ctx->last.launches = launches;
   ctx->last.frames_per_block = fpl;
   ctx->last.stack_window = win ? 1 : 0;
+  ctx->last.quantized = kind == 2 ? 1 : 0;
   ctx->last.workgroups = (int32_t)grid;
   ctx->last_pending = true;
   ctx->last_stats = ctx->stats_on || kDebug || kTiming;

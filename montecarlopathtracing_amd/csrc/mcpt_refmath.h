@@ -30,6 +30,7 @@ constexpr double kClPi = 3.141592653589793115997963468544185161590576171875;  //
 
 __device__ inline float as_f(int32_t i) { return __builtin_bit_cast(float, i); }
 __device__ inline int32_t as_i(float f) { return __builtin_bit_cast(int32_t, f); }
+__device__ inline uint32_t as_u(float f) { return __builtin_bit_cast(uint32_t, f); }
 
 // ------------------------------------------------------------ built-ins
 // dot(float3)/dot(float4): opencl.bc _Z3dotDv3_fS_/_Z3dotDv4_fS_

@@ -210,4 +210,68 @@ int build_sah4(const std::vector<LeafRef> &leaves, std::vector<Node4Rec> &out, i
   return 0;
 }
 
+// ------------------------------------------------------------ quantization
+namespace {
+// the device's decode: one fused multiply-add, one rounding
+inline float qdec(int q, float s, float o) { return std::fma((float)q, s, o); }
+inline bool normal_or_zero(float x) { return x == 0.0f || (std::isfinite(x) && std::fabs(x) >= FLT_MIN); }
+}  // namespace
+
+int quantize_node4(const Node4Rec &in, Node4Q &out) {
+  std::memset(&out, 0, sizeof(out));
+  float scale[3];
+  for (int a = 0; a < 3; ++a) {
+    float lo = FLT_MAX, hi = -FLT_MAX;
+    for (int k = 0; k < 4; ++k) {
+      if (in.link[k] == kEmptySlot4) continue;
+      lo = std::min(lo, in.q[6 * k + 2 * a]);
+      hi = std::max(hi, in.q[6 * k + 2 * a + 1]);
+    }
+    if (lo > hi) lo = hi = 0.0f;  // no slot (cannot happen for built trees)
+    // origin strictly below every lower plane (q = 0 decodes to it exactly),
+    // a normal float or zero (below 0 the next float down would be subnormal)
+    float org = std::nextafter(lo, -FLT_MAX);
+    if (!normal_or_zero(org)) org = -FLT_MIN;
+    if (!normal_or_zero(org) || !std::isfinite(hi)) return -1;
+    // the smallest power of two s with fma(255, s, org) > hi
+    const double span = (double)hi - (double)org;
+    int e = span > 0 ? (int)std::ceil(std::log2(span / 255.0)) : -126;
+    e = std::max(-126, std::min(e, 127));
+    while (e > -126 && qdec(255, std::ldexp(1.0f, e - 1), org) > hi) --e;
+    while (e <= 127 && !(qdec(255, std::ldexp(1.0f, e), org) > hi)) ++e;
+    if (e > 127) return -1;
+    const float s = std::ldexp(1.0f, e);
+    out.org[a] = org;
+    scale[a] = s;
+    for (int k = 0; k < 4; ++k) {
+      uint8_t &ql = out.q[6 * k + 2 * a], &qh = out.q[6 * k + 2 * a + 1];
+      if (in.link[k] == kEmptySlot4) {
+        ql = 0;
+        qh = 0;
+        continue;
+      }
+      const float bl = in.q[6 * k + 2 * a], bh = in.q[6 * k + 2 * a + 1];
+      // lo: the largest q whose decoded plane lies strictly below bl (q = 0 does)
+      int q = (int)std::max(0.0, std::min(255.0, std::floor(((double)bl - (double)org) / s)));
+      while (q > 0 && !(qdec(q, s, org) < bl)) --q;
+      while (q < 255 && qdec(q + 1, s, org) < bl) ++q;
+      while (q > 0 && !normal_or_zero(qdec(q, s, org))) --q;
+      if (!(qdec(q, s, org) < bl) || !normal_or_zero(qdec(q, s, org))) return -1;
+      ql = (uint8_t)q;
+      // hi: the smallest q whose decoded plane lies strictly above bh (q = 255 does)
+      q = (int)std::max(0.0, std::min(255.0, std::ceil(((double)bh - (double)org) / s)));
+      while (q < 255 && !(qdec(q, s, org) > bh)) ++q;
+      while (q > 0 && qdec(q - 1, s, org) > bh) --q;
+      while (q < 255 && !normal_or_zero(qdec(q, s, org))) ++q;
+      if (!(qdec(q, s, org) > bh) || !normal_or_zero(qdec(q, s, org))) return -1;
+      qh = (uint8_t)q;
+    }
+  }
+  out.sx = scale[0];
+  out.sy = scale[1];
+  out.sz = scale[2];
+  for (int k = 0; k < 4; ++k) out.link[k] = in.link[k];
+  return 0;
+}
+
 }  // namespace mcpt

@@ -117,14 +117,15 @@ class Renderer:
     def stats(self):
         s = L.Stats()
         L.check(L.lib().mcpt_get_stats(self.ctx, ctypes.byref(s)))
-        out = {f: getattr(s, f) for f, _ in L.Stats._fields_ if f != "pad"}
+        out = {f: getattr(s, f) for f, _ in L.Stats._fields_ if f not in ("pad", "pad1")}
         out["phase_ticks"] = list(out["phase_ticks"])
         return out
 
     def set_tuning(self, **knobs):
         """mcpt_set_tuning: k_render launch-plan knobs (leaf_threshold,
         shade_threshold, queue_chunk, block_entries, max_block_frames,
-        stack_window 0 auto / 1 window / 2 whole stack, lds_pad, queues); speed only,
+        stack_window 0 auto / 1 window / 2 whole stack, lds_pad, queues, quantized 0 auto / 1
+        the 64-B search-tree nodes / 2 the 128-B ones); speed only,
         unnamed knobs take their defaults."""
         t = L.Tuning()
         for k, v in knobs.items():

@@ -35,7 +35,10 @@ def main():
     cases = [("c1", scenes.cbox(), scenes.CBOX_CAM, w, h, depth, frames, att, g["seeds_in"], {}),
              ("dining", scenes.dining(), scenes.DINING_CAM, 96, 64, 16, 4, 4, None, {}),
              ("c5_window", S.random_mesh(500_000, seed=7), S.RANDOM_MESH_CAMERA, 64, 64, 8, 4, 4, None, {"stack_window": 1}),
-             ("c5_plain", S.random_mesh(500_000, seed=7), S.RANDOM_MESH_CAMERA, 64, 64, 8, 4, 4, None, {"stack_window": 2})]
+             ("c5_plain", S.random_mesh(500_000, seed=7), S.RANDOM_MESH_CAMERA, 64, 64, 8, 4, 4, None, {"stack_window": 2}),
+             ("c1_quant", scenes.cbox(), scenes.CBOX_CAM, w, h, depth, frames, att, g["seeds_in"], {"quantized": 1}),
+             ("c5_window_quant", S.random_mesh(500_000, seed=7), S.RANDOM_MESH_CAMERA, 64, 64, 8, 4, 4, None,
+              {"stack_window": 1, "quantized": 1})]
     for name, data, camj, w, h, depth, frames, att, seeds, tune in cases:
         for mode in (L.MODE_EXACT, L.MODE_NOPRUNE):
             for sched in (L.SCHED_SINGLE, L.SCHED_PAIRED):
@@ -47,7 +50,8 @@ def main():
                 s = rnd.stats()
                 out = {"case": name, "mode": mode, "schedule": sched, "violations": s["debug_violations"],
                        "stack_window": s["stack_window"], "digest": digest(st)}
-                if name == "c1":
+                out["quantized"] = s["quantized"]
+                if name.startswith("c1"):
                     out["golden"] = (st.hist.cpu().numpy().tobytes() == np.ascontiguousarray(g["hist"]).tobytes()
                                      and np.array_equal(st.count.cpu().numpy(), g["count"])
                                      and np.array_equal(st.seeds_np(), g["seeds"]))

@@ -32,6 +32,9 @@ int main(int argc, char **argv) {
       L[i].box[2 * a] = c[a] - e(g);
       L[i].box[2 * a + 1] = c[a] + e(g);
     }
+    if (i % 5 == 1) L[i].box[2 * (i % 3)] = L[i].box[2 * (i % 3) + 1];  // flat on one axis (axis-aligned triangle)
+    if (i % 11 == 2) L[i].box[2 * (i % 3)] = 0.0f, L[i].box[2 * (i % 3) + 1] = std::max(0.0f, L[i].box[2 * (i % 3) + 1]);
+    if (i % 13 == 3) L[i].box[2 * (i % 3) + 1] = 0.0f, L[i].box[2 * (i % 3)] = std::min(0.0f, L[i].box[2 * (i % 3)]);
     L[i].tri = (int)(((long)i * 7919) % n);  // a permutation (n is not a multiple of 7919)
   }
   std::vector<int> leaf_of(n);
@@ -94,6 +97,50 @@ int main(int argc, char **argv) {
     if (seen[i] != 1) return fail("leaf missing", i, seen[i]);
   for (size_t k = 1; k < t1.size(); ++k)
     if (visited[k] != 1) return fail("unreachable node", (long)k, visited[k]);
-  std::printf("ok nodes=%zu need=%d\n", t1.size(), need1);
+  // the 64-B quantized nodes (mcpt::quantize_node4): every decoded slot box
+  // strictly contains the exact one, links unchanged, and the slab test
+  // (objdef.h:223-237, NaN-ignoring fmin/fmax like v_min/v_max_f32) passes on
+  // the decoded box whenever it passes on the exact one -- rays include zero
+  // direction components with the origin exactly on a box plane.
+  std::mt19937 rg(12345u);
+  long slab_checks = 0;
+  for (size_t k = 0; k < t1.size(); ++k) {
+    mcpt::Node4Q qn;
+    if (mcpt::quantize_node4(t1[k], qn) != 0) return fail("quantize", (long)k, 0);
+    const float s[3] = {qn.sx, qn.sy, qn.sz};
+    for (int c = 0; c < 4; ++c) {
+      if (qn.link[c] != t1[k].link[c]) return fail("quantized link", (long)k, c);
+      if (t1[k].link[c] == mcpt::kEmptySlot4) continue;
+      const float *b = t1[k].q + 6 * c;
+      float dq[6];
+      for (int i = 0; i < 6; ++i) dq[i] = std::fma((float)qn.q[6 * c + i], s[i / 2], qn.org[i / 2]);
+      for (int a = 0; a < 3; ++a)
+        if (!(dq[2 * a] < b[2 * a]) || !(dq[2 * a + 1] > b[2 * a + 1])) return fail("not strictly contained", (long)k, c);
+      for (int r = 0; r < 24; ++r) {
+        float o[3], d[3];
+        for (int a = 0; a < 3; ++a) {
+          const int pick = (int)(rg() % 6);  // origin on a plane, inside, or anywhere
+          o[a] = pick == 0 ? b[2 * a] : pick == 1 ? b[2 * a + 1] : pick == 2 ? 0.5f * (b[2 * a] + b[2 * a + 1])
+                                                                              : (float)((int)(rg() % 200) - 100);
+          const int dz = (int)(rg() % 4);  // +0, -0, or a random component
+          d[a] = dz == 0 ? 0.0f : dz == 1 ? -0.0f : (float)((int)(rg() % 2001) - 1000) / 1000.0f;
+        }
+        auto pass = [&](const float *bx) {
+          float tn = -INFINITY, tf = INFINITY;
+          for (int a = 0; a < 3; ++a) {
+            const float ri = 1.0f / d[a];
+            const float t1 = (bx[2 * a] - o[a]) * ri, t2 = (bx[2 * a + 1] - o[a]) * ri;
+            const float mn = std::fmin(t1, t2), mx = std::fmax(t1, t2);
+            tn = a == 0 ? mn : std::fmax(tn, mn);
+            tf = a == 0 ? mx : std::fmin(tf, mx);
+          }
+          return !(tf < tn || tf < 0.001f);
+        };
+        ++slab_checks;
+        if (pass(b) && !pass(dq)) return fail("decoded box fails where the exact box passes", (long)k, c);
+      }
+    }
+  }
+  std::printf("ok nodes=%zu need=%d slab_checks=%ld\n", t1.size(), need1, slab_checks);
   return 0;
 }

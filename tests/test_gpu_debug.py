@@ -4,8 +4,9 @@ stack's capacity and every node / triangle index against its array.  The
 reference traversal keeps an unchecked int stack[64] (objdef.h:247); here the
 bound computed at upload is verified at run time on the C1
 image, the deep diningroom proxy and the C5 random mesh with both stack
-layouts, both modes and both leaf schedules: zero violations, C1 still equal
-to the reference kernels' golden image, and the two stack layouts bit-identical."""
+layouts, both search-tree node formats, both modes and both leaf schedules:
+zero violations, C1 still equal to the reference kernels' golden image, and
+the stack layouts and node formats bit-identical."""
 import json
 import os
 import subprocess
@@ -28,10 +29,13 @@ def test_debug_build_bounds_checks_clean():
     lines = [json.loads(x) for x in r.stdout.splitlines() if x.startswith("{")]
     assert "MCPT_DEBUG" in lines[0]["version"]
     cases = lines[1:]
-    assert len(cases) == 16
+    assert len(cases) == 24
     for c in cases:
         assert c["violations"] == 0, c
-    assert all(c["golden"] for c in cases if c["case"] == "c1")
+    assert all(c["golden"] for c in cases if c["case"] in ("c1", "c1_quant"))
+    # EXACT mode searched the quantized tree where forced (NOPRUNE never does)
+    assert {c["quantized"] for c in cases if c["case"].endswith("_quant") and c["mode"] == 0} == {1}
+    assert {c["quantized"] for c in cases if not c["case"].endswith("_quant") or c["mode"] == 1} == {0}
     assert {c["stack_window"] for c in cases if c["case"] == "c5_window"} == {1}
     assert {c["stack_window"] for c in cases if c["case"] == "c5_plain"} == {0}
     for mode in (0, 1):
@@ -41,3 +45,6 @@ def test_debug_build_bounds_checks_clean():
             assert win[0]["digest"] == plain[0]["digest"]
     for name in ("c1", "dining", "c5_window"):
         assert len({c["digest"] for c in cases if c["case"] == name}) == 1  # modes and schedules agree
+    for name in ("c1", "c5_window"):  # node formats agree
+        assert {c["digest"] for c in cases if c["case"] == name + "_quant"} == {c["digest"] for c in cases
+                                                                               if c["case"] == name}

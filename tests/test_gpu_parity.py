@@ -155,6 +155,64 @@ def test_render_frames_bitexact(rnd, name, getter, camjson, depth, schedule):
 
 
 @needs_ref
+@pytest.mark.parametrize("name,getter,camjson,depth", [("cbox", scenes.cbox, scenes.CBOX_CAM, 4),
+                                                       ("mis", scenes.mis, scenes.MIS_CAM, 12),
+                                                       ("dining", scenes.dining, scenes.DINING_CAM, 16)])
+@pytest.mark.parametrize("schedule", [L.SCHED_SINGLE, L.SCHED_PAIRED])
+@pytest.mark.parametrize("quantized", [1, 2])
+def test_render_node_formats_bitexact(rnd, name, getter, camjson, depth, schedule, quantized):
+    """Both search-tree node formats, forced: the 64-B quantized nodes (decoded
+    boxes strictly larger than the exact ones, the leaf's exact box re-tested
+    in the L phase; auto-picked for trees beyond the L2) and the 128-B exact
+    nodes match the reference kernels bit for bit."""
+    rnd.set_tuning(quantized=quantized)
+    try:
+        (h_, c_, s_), (rh, rc, rs) = _render_both(rnd, getter(), camjson, 64, 64, depth, 4, 4, schedule=schedule)
+        assert rnd.stats()["quantized"] == (1 if quantized == 1 else 0)
+    finally:
+        rnd.set_tuning()
+    assert_bits_equal(c_, rc, "count")
+    assert_bits_equal(s_, rs, "seeds")
+    assert_bits_equal(h_, rh, "hist")
+
+
+@needs_ref
+def test_padded_leaf_boxes_keep_full_nodes_bitexact(rnd):
+    """A tree whose leaf boxes are not the triangles' vertex bounds (a foreign
+    BVH with padded leaves) cannot use the L phase's rebuilt leaf box: the scene
+    keeps the 128-B nodes only, and still matches the reference kernels over the
+    same padded tree."""
+    data = scenes.cbox()
+    nodes = data.nodes.copy()
+    leaves = np.flatnonzero(nodes["left"] == nodes["right"])
+    pad = leaves[::7]
+    nodes["bbmin"][pad, :3] -= 0.25
+    nodes["bbmax"][pad, :3] += 0.25
+    # refit the internal boxes (unions again), so the tree stays a valid BVH
+    order, stack = [], [0]
+    while stack:
+        k = stack.pop()
+        order.append(k)
+        if nodes["left"][k] != nodes["right"][k]:
+            stack += [int(nodes["left"][k]), int(nodes["right"][k])]
+    for k in reversed(order):
+        l, r = nodes["left"][k], nodes["right"][k]
+        if l != r:
+            nodes["bbmin"][k] = np.minimum(nodes["bbmin"][l], nodes["bbmin"][r])
+            nodes["bbmax"][k] = np.maximum(nodes["bbmax"][l], nodes["bbmax"][r])
+    data = data.with_nodes(nodes)
+    rnd.set_tuning(quantized=1)
+    try:
+        (h_, c_, s_), (rh, rc, rs) = _render_both(rnd, data, scenes.CBOX_CAM, 64, 64, 6, 4, 4)
+        assert rnd.stats()["quantized"] == 0
+    finally:
+        rnd.set_tuning()
+    assert_bits_equal(c_, rc, "count")
+    assert_bits_equal(s_, rs, "seeds")
+    assert_bits_equal(h_, rh, "hist")
+
+
+@needs_ref
 @pytest.mark.parametrize("name,getter,camjson,depth", [("cbox", scenes.cbox, scenes.CBOX_CAM, 6),
                                                        ("mis", scenes.mis, scenes.MIS_CAM, 12)])
 def test_render_over_treelet_bvh_bitexact(rnd, name, getter, camjson, depth):
@@ -175,17 +233,21 @@ NEAR_TIES = [("cbox", 0.0, scenes.CBOX_CAM), ("mis", 0.0, scenes.MIS_CAM), ("mis
 
 @needs_ref
 @pytest.mark.parametrize("name,offset,camjson", NEAR_TIES)
-def test_near_ties_bitexact(rnd, name, offset, camjson):
+@pytest.mark.parametrize("quantized", [1, 2])
+def test_near_ties_bitexact(rnd, name, offset, camjson, quantized):
     """Twin triangles less than EPS apart: the nearest-first search must hand
-    these rays to the reference-order search and still match bit for bit."""
+    these rays to the reference-order search and still match bit for bit
+    (with either search-tree node format)."""
     data = scenes.near_ties(name, offset)
     _bounce_chain(rnd, data, camjson, 48, 40, 4, L.MODE_EXACT)
     rnd.set_stats(True)
+    rnd.set_tuning(quantized=quantized)
     try:
         (h_, c_, s_), (rh, rc, rs) = _render_both(rnd, data, camjson, 64, 64, 6, 4, 4)
         fallbacks = rnd.stats()["order_fallbacks"]
     finally:
         rnd.set_stats(False)
+        rnd.set_tuning()
     assert_bits_equal(c_, rc, "count")
     assert_bits_equal(s_, rs, "seeds")
     assert_bits_equal(h_, rh, "hist")
@@ -256,11 +318,12 @@ def test_frame_blocks_handoff_full_size(rnd):
 @pytest.mark.parametrize("name,getter,camjson,depth", [("cbox", scenes.cbox, scenes.CBOX_CAM, 8),
                                                        ("dining", scenes.dining, scenes.DINING_CAM, 16)])
 @pytest.mark.parametrize("schedule", [L.SCHED_SINGLE, L.SCHED_PAIRED])
-def test_render_windowed_stack_bitexact(rnd, name, getter, camjson, depth, schedule):
+@pytest.mark.parametrize("quantized", [1, 2])
+def test_render_windowed_stack_bitexact(rnd, name, getter, camjson, depth, schedule, quantized):
     """The LDS-window stack (top 32 entries in LDS, the rest spilled to a
     per-lane global area; picked at launch for deep trees) is the same
     logical stack: forced on, renders still match the reference bit for bit."""
-    rnd.set_tuning(stack_window=1)
+    rnd.set_tuning(stack_window=1, quantized=quantized)
     try:
         (h_, c_, s_), (rh, rc, rs) = _render_both(rnd, getter(), camjson, 64, 64, depth, 4, 4, schedule=schedule)
     finally:
@@ -339,7 +402,8 @@ def _c5_small():
 
 @needs_ref
 @pytest.mark.parametrize("schedule", [L.SCHED_SINGLE, L.SCHED_PAIRED])
-def test_random_mesh_c5_bitexact(rnd, schedule):
+@pytest.mark.parametrize("quantized", [1, 2])
+def test_random_mesh_c5_bitexact(rnd, schedule, quantized):
     """C5 (the deep-BVH random mesh): 500 K triangles at 64x64, depth 8, 5
     frames, with the launch plan on auto (the stack layout picked by the
     occupancy rule, not forced; the frames split into blocks handed between
@@ -349,8 +413,13 @@ def test_random_mesh_c5_bitexact(rnd, schedule):
     bit."""
     data = _c5_small()
     assert S.bvh_stack_depth(data.nodes) <= 64  # within the reference's stack
-    (h_, c_, s_), (rh, rc, rs) = _render_both(rnd, data, S.RANDOM_MESH_CAMERA, 64, 64, 8, 5, 4, schedule=schedule)
-    st = rnd.stats()
+    rnd.set_tuning(quantized=quantized)
+    try:
+        (h_, c_, s_), (rh, rc, rs) = _render_both(rnd, data, S.RANDOM_MESH_CAMERA, 64, 64, 8, 5, 4, schedule=schedule)
+        st = rnd.stats()
+    finally:
+        rnd.set_tuning()
+    assert st["quantized"] == (1 if quantized == 1 else 0)
     assert st["frames_per_block"] < 5 and st["stack_window"] in (0, 1)  # >= 2 blocks: a hand-off happened
     assert_bits_equal(c_, rc, "count")
     assert_bits_equal(s_, rs, "seeds")
@@ -361,22 +430,28 @@ def test_random_mesh_c5_bitexact(rnd, schedule):
 def test_random_mesh_c5_full_size_properties(rnd):
     """C5 at its full size: 10 M random triangles, the HLBVH built on the GPU
     (mcpt_build_hlbvh_device), 2048x2048, depth 8, 2 frames.  Size-independent
-    properties: one 2-frame block, two 1-frame blocks handed between lanes,
-    and the rows split into 3 GPUs' stripes rendered in turn give the same
-    bits; radiance is finite and non-negative, counts are within [0, 2] and
-    some pixels see the light."""
+    properties: one 2-frame block (the auto plan: the quantized search tree,
+    this tree being far beyond the L2), two 1-frame blocks handed between
+    lanes, the rows split into 3 GPUs' stripes rendered in turn, and the
+    128-B exact nodes give the same bits; radiance is finite and
+    non-negative, counts are within [0, 2] and some pixels see the light."""
     data = S.random_mesh(10_000_000, build=R.build_hlbvh_host_nodes)
     cam = S.parse_camera(S.RANDOM_MESH_CAMERA)
     w = h = 2048
     seeds = R.default_seeds(w * h)
     dsc = rnd.upload(data)
     outs = []
-    for stripes, fpl in ((1, 2), (1, 1), (3, 1)):
+    for stripes, fpl, quantized in ((1, 2, 0), (1, 1, 0), (3, 1, 0), (1, 2, 2)):
         st = rnd.new_state(w, h, seeds)
-        for k in range(stripes):
-            rnd.render_frames(dsc, cam, st, 8, 1 << 20, 2, stripe_rows=16, stripe_index=k, stripe_count=stripes,
-                              frames_per_launch=fpl)
-        torch.cuda.synchronize()
+        rnd.set_tuning(quantized=quantized)
+        try:
+            for k in range(stripes):
+                rnd.render_frames(dsc, cam, st, 8, 1 << 20, 2, stripe_rows=16, stripe_index=k, stripe_count=stripes,
+                                  frames_per_launch=fpl)
+            torch.cuda.synchronize()
+            assert rnd.stats()["quantized"] == (1 if quantized == 0 else 0)
+        finally:
+            rnd.set_tuning()
         outs.append((st.hist.cpu().numpy(), st.count.cpu().numpy(), st.seeds_np()))
     dsc.close()
     for o in outs[1:]:

@@ -98,6 +98,7 @@ def main():
             seg = max(c["segments"], 1)
             rec.update({"segments": c["segments"], "node_per_seg": round(c["node_visits"] / seg, 3),
                         "tri_per_seg": round(c["tri_tests"] / seg, 3),
+                        "leaf_rejects_per_seg": round(c.get("leaf_rejects", 0) / seg, 3),
                         "simt_T": round(c["node_visits"] / (64.0 * max(c["wave_node_phases"], 1)), 3),
                         "simt_L": round(c["tri_tests"] / (64.0 * max(c["wave_leaf_phases"], 1)), 3),
                         "simt_S": round(seg / (64.0 * max(c["wave_shade_phases"], 1)), 3),
