@@ -256,6 +256,7 @@ def main():
     kst = rnd.stats()
     kernel_ms, launches = kst["kernel_ms"], max(kst["launches"], 1)
     fpb = kst["frames_per_block"]
+    search_tree = "64-B quantized" if kst.get("quantized") else "128-B exact"
 
     # replay the same frames with counters on (deterministic: same segments)
     # (the counting kernel runs the replay's warmup too, so the timed launch
@@ -306,7 +307,8 @@ def main():
         seg_per_launch = segments / float(launches)
         prof = load_profile(args.workload, args.steps) if n == 1 else None
         roof = {"bound": "hbm", "peak": HBM_PEAK_GBS, "unit": "GB/s", "achieved": None, "frac": None, "traffic": None,
-                "kernel": "k_render<EXACT, no stats, %s>" % ("paired" if dsc.schedule == L.SCHED_PAIRED else "single"),
+                "kernel": "k_render<EXACT, no stats, %s, %s nodes>" % (
+                    "paired" if dsc.schedule == L.SCHED_PAIRED else "single", search_tree),
                 "avg_launch_ms": round(avg_launch_s * 1e3, 3), "segments_per_launch": int(seg_per_launch),
                 "kernel_node_fetches_per_seg": round(cst["node_visits"] / max(segments, 1), 3),
                 "kernel_tri_tests_per_seg": round(cst["tri_tests"] / max(segments, 1), 3)}
@@ -316,7 +318,9 @@ def main():
             roof["achieved"] = round(traffic / avg_launch_s / 1e9, 2)
             roof["frac"] = round(roof["achieved"] / HBM_PEAK_GBS, 5)
             roof["issue_frac"] = prof.get("valu_busy")
-            roof["binding"] = "gather latency + VALU issue (cache-resident scene; see DESIGN.md §3.6)"
+            roof["td_busy"] = prof.get("td_busy")
+            roof["binding"] = ("vector-memory gathers: TD (data-return) busy %s of the kernel's cycles, VALU issue %s "
+                               "(DESIGN.md §3.6; profiles/r02_probe_ab.txt)" % (prof.get("td_busy"), prof.get("valu_busy")))
             for k in ("l1_hit_rate", "l2_hit_rate", "l2_hit_GBps_128B_lines", "wave_wait_any_per_wave_cycle",
                       "gather_latency_cycles_per_vmem_rd", "fetch_scale_calibrated", "timed_launch_ms_rocprof"):
                 roof[k] = prof.get(k)
@@ -344,7 +348,7 @@ def main():
                           "width": W, "height": h_img, "max_depth": DEPTH,
                           "parallelism": "row-stripe tiles x%d" % n, "mode": "exact",
                           "schedule": "paired" if dsc.schedule == L.SCHED_PAIRED else "single",
-                          "frames_per_block": fpb},
+                          "frames_per_block": fpb, "search_tree_nodes": search_tree},
                "active_Msegments_per_s": round(segments * n / elapsed / 1e6, 2),
                "image_reduce_ms": None if reduce_ms is None else round(reduce_ms, 3),
                "weak_scaling": weak,

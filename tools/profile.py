@@ -127,7 +127,8 @@ def summarize(tag):
     shutil.copy(stats_csv, os.path.join(dst, tag + "_kernel_stats.csv"))
     shutil.copy(trace_csv, os.path.join(dst, tag + "_kernel_trace.csv"))
     sched = bench["config"]["schedule"]
-    kname = r"k_render<0, false, (false|true), %s>" % ("true" if sched == "paired" else "false")
+    quant = "true" if bench["config"].get("search_tree_nodes", "").startswith("64") else "false"
+    kname = r"k_render<0, false, (false|true), %s, %s>" % ("true" if sched == "paired" else "false", quant)
     trace = [r for r in csv.DictReader(open(trace_csv)) if re.search(kname, r["Kernel_Name"])]
     timed = trace[-1]
     timed_ms = (int(timed["End_Timestamp"]) - int(timed["Start_Timestamp"])) / 1e6
@@ -198,6 +199,9 @@ def summarize(tag):
         "l2_hit_GBps_128B_lines": round(ctr["TCC_HIT_sum"] * 128.0 / secs / 1e9, 1),
         "gather_latency_cycles_per_vmem_rd": round(ctr["TCP_TCP_LATENCY_sum"] / max(ctr["SQ_INSTS_VMEM_RD"], 1), 1),
         "ta_busy_sum": ctr.get("TA_TA_BUSY_sum"), "td_busy_sum": ctr.get("TD_TD_BUSY_sum"),
+        # vector-memory address (TA) and data-return (TD) units: busy cycles per CU per kernel cycle
+        "ta_busy": round(ctr.get("TA_TA_BUSY_sum", float("nan")) / (N_CU * cycles), 4),
+        "td_busy": round(ctr.get("TD_TD_BUSY_sum", float("nan")) / (N_CU * cycles), 4),
         "counters_timed_dispatch": ctr,
         "sources": ["profiles/%s_%s.csv" % (tag, x) for x in
                     ["kernel_stats", "kernel_trace"] + ["pmc_" + n for n in PASSES] + ["calib_fetch", "calib_write"]],
@@ -217,6 +221,7 @@ def summarize(tag):
     allw = {k: v for k, v in allw.items() if "@" in k}  # drop the round-1 layout
     allw[key] = {"hbm_bytes_per_launch": rd + wr, "hbm_read_bytes_per_launch": rd, "hbm_write_bytes_per_launch": wr,
                  "fetch_scale_calibrated": summ["fetch_scale_calibrated"], "valu_busy": summ["valu_busy"],
+                 "ta_busy": summ["ta_busy"], "td_busy": summ["td_busy"],
                  "wave_wait_any_per_wave_cycle": summ["wave_wait_any_per_wave_cycle"],
                  "l2_hit_rate": summ["l2_hit_rate"], "l1_hit_rate": summ["l1_hit_rate"],
                  "l2_hit_GBps_128B_lines": summ["l2_hit_GBps_128B_lines"],
