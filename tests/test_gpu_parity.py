@@ -405,9 +405,8 @@ def _c5_small():
 @pytest.mark.parametrize("quantized", [1, 2])
 def test_random_mesh_c5_bitexact(rnd, schedule, quantized):
     """C5 (the deep-BVH random mesh): 500 K triangles at 64x64, depth 8, 5
-    frames, with the launch plan on auto (the stack layout picked by the
-    occupancy rule, not forced; the frames split into blocks handed between
-    lanes).
+    frames, the stack layout on auto (picked by the occupancy rule, not
+    forced), the frames in 2-frame blocks handed between lanes.
     The reference's own kernels traverse the same tree with their fixed
     int stack[64] (objdef.h:247); images, counts and seeds match bit for
     bit."""
@@ -415,12 +414,13 @@ def test_random_mesh_c5_bitexact(rnd, schedule, quantized):
     assert S.bvh_stack_depth(data.nodes) <= 64  # within the reference's stack
     rnd.set_tuning(quantized=quantized)
     try:
-        (h_, c_, s_), (rh, rc, rs) = _render_both(rnd, data, S.RANDOM_MESH_CAMERA, 64, 64, 8, 5, 4, schedule=schedule)
+        (h_, c_, s_), (rh, rc, rs) = _render_both(rnd, data, S.RANDOM_MESH_CAMERA, 64, 64, 8, 5, 4, schedule=schedule,
+                                                  frames_per_launch=2)
         st = rnd.stats()
     finally:
         rnd.set_tuning()
     assert st["quantized"] == (1 if quantized == 1 else 0)
-    assert st["frames_per_block"] < 5 and st["stack_window"] in (0, 1)  # >= 2 blocks: a hand-off happened
+    assert st["frames_per_block"] == 2 and st["stack_window"] in (0, 1)  # 3 blocks: hand-offs happened
     assert_bits_equal(c_, rc, "count")
     assert_bits_equal(s_, rs, "seeds")
     assert_bits_equal(h_, rh, "hist")
