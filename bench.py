@@ -127,7 +127,7 @@ def cpu_quota():
         return None
 
 
-def cpu_baseline(data, cam, h_img, target_s=15.0):
+def cpu_baseline(data, cam, h_img, target_s=15.0, label="C2"):
     """The CPU oracle on a bounded sample: every k-th pixel of the same image,
     same depth, frames scaled so the sample takes ~target_s seconds, on every
     core this process may run on (all host cores)."""
@@ -159,9 +159,9 @@ def cpu_baseline(data, cam, h_img, target_s=15.0):
     return {"value": len(px) * frames * DEPTH / dt / 1e6, "unit": "Msamples/s", "cores": threads,
             "kind": "port", "nproc": os.cpu_count(), "affinity_cpus": affinity, "cgroup_cpu_quota": quota, "omp_num_threads_env": omp,
             "cpu_model": cpu_model(), "threads": threads,
-            "sample": "every %dth pixel (%d px) of the 1024x1024 C2 image x %d frames x depth %d, %.1f s; "
+            "sample": "every %dth pixel (%d px) of the %dx%d %s image x %d frames x depth %d, %.1f s; "
                       "oracle/mcpt_oracle.c exhaustive reference traversal, %d OpenMP threads" % (
-                          stride, len(px), frames, DEPTH, dt, threads),
+                          stride, len(px), W, h_img, label, frames, DEPTH, dt, threads),
             "active_Msegments_per_s": float(st[0]) / dt / 1e6}
 
 
