@@ -246,9 +246,11 @@ def main():
     kw = dict(stripe_rows=STRIPE_ROWS, stripe_index=rank, stripe_count=n, frames_per_launch=args.frames_per_launch)
     attempt = 1 << 30
     # leaf-test schedule (identical images; speed only), chosen before any timing
+    shade_th = rnd.get_tuning()["shade_threshold"] or 32
     if args.schedule == "auto":
         # timed on calls of the timed call's size (same frame-block regime), 3 trials each
-        rnd.tune_schedule(dsc, cam, st, DEPTH, attempt, frames=max(1, min(args.steps, 64)), trials=3, **kw)
+        # and the S-phase threshold (speed only; every setting gives the same bits)
+        _, shade_th, _ = rnd.tune(dsc, cam, st, DEPTH, attempt, frames=max(1, min(args.steps, 64)), trials=3, **kw)
     else:
         dsc.schedule = L.SCHED_PAIRED if args.schedule == "paired" else L.SCHED_SINGLE
 
@@ -348,6 +350,7 @@ def main():
                           "width": W, "height": h_img, "max_depth": DEPTH,
                           "parallelism": "row-stripe tiles x%d" % n, "mode": "exact",
                           "schedule": "paired" if dsc.schedule == L.SCHED_PAIRED else "single",
+                          "shade_threshold": shade_th,
                           "frames_per_block": fpb, "search_tree_nodes": search_tree},
                "active_Msegments_per_s": round(segments * n / elapsed / 1e6, 2),
                "image_reduce_ms": None if reduce_ms is None else round(reduce_ms, 3),

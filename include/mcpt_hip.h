@@ -176,9 +176,11 @@ typedef struct mcpt_stats {
  * keeps its default.  Replaces the environment knobs of earlier builds:
  * nothing is read from the environment on the render path. */
 typedef struct mcpt_tuning {
-  int32_t leaf_threshold;   /* lanes with a pending leaf before the L phase runs
-                               (default 4 single / 16 paired schedule)          */
-  int32_t shade_threshold;  /* lanes waiting before the S phase runs (32)        */
+  int32_t leaf_threshold;   /* lanes with a pending leaf before the L phase runs,
+                               for a wave of 64 live lanes (default 4 single /
+                               16 paired schedule; scaled to the live lanes)   */
+  int32_t shade_threshold;  /* lanes waiting before the S phase runs, for 64
+                               live lanes (32; scaled the same way)            */
   int32_t queue_chunk;      /* queue entries a wave claims per atomic (4)        */
   int32_t block_entries;    /* auto frames-per-block: smallest block count that
                                gives every resident lane this many queue entries

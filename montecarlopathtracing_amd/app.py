@@ -71,8 +71,9 @@ class App:
             self.init()
         att = self.cfg.MAXATTEPMT()
         todo = frames
-        if frames >= 4096 and not getattr(self, "_tuned", False):  # long runs (tuning costs 128 frames): time both leaf schedules
-            self.renderer.tune_schedule(self.scene, self.camera, self.state, self.cfg.MAXDEPTH(), att)
+        if frames >= 4096 and not getattr(self, "_tuned", False):  # long runs: time the leaf schedules and S-phase
+            # thresholds on 16-frame calls (96 scratch frames, bit-identical either way)
+            self.renderer.tune(self.scene, self.camera, self.state, self.cfg.MAXDEPTH(), att, frames=16)
             self._tuned = True
         while todo > 0:
             n = todo if self.attempt_count > att else min(todo, att + 1 - self.attempt_count)

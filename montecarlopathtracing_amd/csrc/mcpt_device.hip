@@ -883,6 +883,12 @@ __global__ void __launch_bounds__(64, MCPT_WAVES_PER_SIMD) k_render(RenderArgs A
     MCPT_TICK(0);
     if (!__ballot(lst != kDead)) break;
     const bool live = lst == kBusy;
+    // phase thresholds scaled to the wave's live lanes: a wave with few pixels
+    // (a launch's tail, a strong-scaled rank) does not wait for lane counts
+    // only a full wave reaches (C2 -3 %, C5 -4 %, C2 4- and 8-rank shares
+    // -16 % / -19 %; profiles/r02_shares_calls.txt)
+    const int n_live = __popcll(__ballot(live));
+    const int th_leaf = max(1, (A.th_leaf * n_live + 63) >> 6), th_shade = max(1, (A.th_shade * n_live + 63) >> 6);
     if (STATS) {
       if (lane == __builtin_ctzll(__ballot(1))) w_it++;
       n_wait += lst == kPend;
@@ -975,7 +981,7 @@ __global__ void __launch_bounds__(64, MCPT_WAVES_PER_SIMD) k_render(RenderArgs A
     // ---- L: triangle tests, batched
     const bool in_l = live && cur < 0 && cur != kDone;
     const unsigned long long ml = __ballot(in_l);
-    if (ml && (__popcll(ml) >= A.th_leaf || !__ballot(live && cur >= 0))) {
+    if (ml && (__popcll(ml) >= th_leaf || !__ballot(live && cur >= 0))) {
       if (STATS && lane == __builtin_ctzll(__ballot(1))) w_l++;
       if (in_l) {
         // PAIR (MCPT_SCHED_PAIRED): when the next stack entry is a leaf too,
@@ -1035,7 +1041,7 @@ __global__ void __launch_bounds__(64, MCPT_WAVES_PER_SIMD) k_render(RenderArgs A
     // ---- S: finish the segment (shade.cl), accumulate (history.cl), next segment
     const bool in_s = live && cur == kDone;
     const unsigned long long ms = __ballot(in_s);
-    if (ms && (__popcll(ms) >= A.th_shade || !__ballot(live && cur != kDone))) {
+    if (ms && (__popcll(ms) >= th_shade || !__ballot(live && cur != kDone))) {
       if (STATS && lane == __builtin_ctzll(__ballot(1))) w_s++;
       if (in_s && !ref && near_ambiguous(best_t, t2)) {  // order could matter: search again left-first
         if (STATS) n_fb++;

@@ -61,8 +61,8 @@ def render_distributed(renderer, scene, camera, width, height, max_depth, max_at
     rank, world = dist.get_rank(group), dist.get_world_size(group)
     st = renderer.new_state(width, height, seeds)
     kw = dict(stripe_rows=stripe_rows, stripe_index=rank, stripe_count=world, mode=mode)
-    if frames >= 4096:  # long runs (tuning costs 128 frames): each rank times both leaf-test schedules (same bits)
-        renderer.tune_schedule(scene, camera, st, max_depth, max_attempt, **kw)
+    if frames >= 4096:  # long runs: each rank times the leaf schedules and S-phase thresholds (same bits)
+        renderer.tune(scene, camera, st, max_depth, max_attempt, frames=16, **kw)
     renderer.render_frames(scene, camera, st, max_depth, max_attempt, frames, **kw)
     torch.cuda.synchronize()
     mask = ownership_mask(width, height, stripe_rows, rank, world)

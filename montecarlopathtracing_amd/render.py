@@ -191,20 +191,42 @@ class Renderer:
         of `state` (interleaved, device time of each call), keep the faster
         in scene.schedule.  Both schedules give bit-identical images, so this
         only moves speed.  Returns (schedule, {schedule: best ms})."""
+        sched, _, best = self.tune(scene, camera, state, max_depth, max_attempt, frames, trials, shade_thresholds=None,
+                                   **kw)
+        return sched, {k[0]: v for k, v in best.items()}
+
+    def tune(self, scene, camera, state, max_depth, max_attempt, frames=64, trials=1, shade_thresholds=(32, 40, 48),
+             **kw):
+        """tune_schedule over the leaf-test schedule AND the S-phase threshold
+        (mcpt_tuning.shade_threshold; the best differs by scene: veach_mis 48,
+        cbox 40, the 10 M-triangle soup 32).  Every combination gives the same
+        bits.  The winner goes to scene.schedule and the renderer's tuning.
+        Returns (schedule, shade_threshold, {(schedule, threshold): best ms})."""
         if getattr(self, "_stats_on", False):
-            raise L.MCPTError("tune_schedule: counters must be off (they change the kernel)")
+            raise L.MCPTError("tune: counters must be off (they change the kernel)")
+        base = self.get_tuning()
+        ths = list(shade_thresholds) if shade_thresholds else [base["shade_threshold"]]
         scratch = ImageState.__new__(ImageState)
         scratch.width, scratch.height, scratch.frames_done = state.width, state.height, state.frames_done
         best = {}
-        for _ in range(int(trials)):
-            for sched in (L.SCHED_SINGLE, L.SCHED_PAIRED):
-                scratch.seeds, scratch.hist, scratch.count = state.seeds.clone(), state.hist.clone(), state.count.clone()
-                self.render_frames(scene, camera, scratch, max_depth, max_attempt, frames,
-                                   frame_begin=state.frames_done, schedule=sched, **kw)
-                ms = self.stats()["kernel_ms"]
-                best[sched] = min(best.get(sched, ms), ms)
-        scene.schedule = min(best, key=lambda k: (best[k], k))
-        return scene.schedule, best
+        try:
+            for _ in range(int(trials)):
+                for th in ths:
+                    self.set_tuning(**dict(base, shade_threshold=th))
+                    for sched in (L.SCHED_SINGLE, L.SCHED_PAIRED):
+                        scratch.seeds, scratch.hist, scratch.count = (state.seeds.clone(), state.hist.clone(),
+                                                                      state.count.clone())
+                        self.render_frames(scene, camera, scratch, max_depth, max_attempt, frames,
+                                           frame_begin=state.frames_done, schedule=sched, **kw)
+                        ms = self.stats()["kernel_ms"]
+                        best[(sched, th)] = min(best.get((sched, th), ms), ms)
+        finally:
+            self.set_tuning(**base)
+        sched, th = min(best, key=lambda k: (best[k], k))
+        scene.schedule = sched
+        if shade_thresholds:
+            self.set_tuning(**dict(base, shade_threshold=th))
+        return sched, th, best
 
     # ------------------------------------------------ wavefront (drop-in)
     def generate_rays(self, camera, width, height):

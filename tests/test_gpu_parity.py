@@ -376,6 +376,18 @@ def test_tune_schedule_leaves_state_alone(rnd):
         assert_bits_equal(a, b, what)
     with pytest.raises(L.MCPTError):
         rnd.render_frames(dsc, cam, st, 12, 1 << 20, 1, schedule=7)
+    # the combined tuning (schedule x S-phase threshold) leaves the state alone too
+    st2 = rnd.new_state(w, h, seeds)
+    sched, th, best2 = rnd.tune(dsc, cam, st2, 12, 1 << 20, frames=4, trials=1)
+    try:
+        assert th in (32, 40, 48) and rnd.get_tuning()["shade_threshold"] == th and dsc.schedule == sched
+        assert len(best2) == 6 and int(st2.count.sum()) == 0
+        rnd.render_frames(dsc, cam, st2, 12, 1 << 20, 6)
+        torch.cuda.synchronize()
+        assert_bits_equal(st2.hist.cpu().numpy(), ref.hist.cpu().numpy(), "hist after tune")
+        assert_bits_equal(st2.seeds_np(), ref.seeds_np(), "seeds after tune")
+    finally:
+        rnd.set_tuning()
     dsc.close()
 
 
