@@ -212,6 +212,9 @@ def main():
     ap.add_argument("--schedule", default="auto", choices=["auto", "single", "paired"],
                     help="k_render leaf-test schedule; auto times both before the warmup (untimed)")
     ap.add_argument("--no-weak", action="store_true", help="N > 1: skip the weak-scaling leg")
+    ap.add_argument("--shade-threshold", type=int, default=0,
+                    help="k_render S-phase threshold (mcpt_tuning.shade_threshold); 0: tuned with the schedule "
+                         "when --schedule is auto, else the default")
     args = ap.parse_args()
     global W, H_PER_GPU, DEPTH
     wl = WORKLOADS[args.workload]
@@ -246,8 +249,12 @@ def main():
     kw = dict(stripe_rows=STRIPE_ROWS, stripe_index=rank, stripe_count=n, frames_per_launch=args.frames_per_launch)
     attempt = 1 << 30
     # leaf-test schedule (identical images; speed only), chosen before any timing
+    if args.shade_threshold > 0:
+        rnd.set_tuning(**dict(rnd.get_tuning(), shade_threshold=args.shade_threshold))
     shade_th = rnd.get_tuning()["shade_threshold"] or 32
-    if args.schedule == "auto":
+    if args.schedule == "auto" and args.shade_threshold > 0:
+        rnd.tune_schedule(dsc, cam, st, DEPTH, attempt, frames=max(1, min(args.steps, 64)), trials=3, **kw)
+    elif args.schedule == "auto":
         # timed on calls of the timed call's size (same frame-block regime), 3 trials each
         # and the S-phase threshold (speed only; every setting gives the same bits)
         _, shade_th, _ = rnd.tune(dsc, cam, st, DEPTH, attempt, frames=max(1, min(args.steps, 64)), trials=3, **kw)

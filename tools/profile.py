@@ -73,8 +73,8 @@ def run(tag, args):
     print(line[-600:], flush=True)
     # the same command with the schedule the bench line's tuning picked, so
     # every pass profiles the same kernel instantiation
-    sched = json.loads(line.splitlines()[-1])["config"]["schedule"]
-    quiet = bench + ["--no-cpu", "--schedule", sched]
+    cfg = json.loads(line.splitlines()[-1])["config"]
+    quiet = bench + ["--no-cpu", "--schedule", cfg["schedule"], "--shade-threshold", str(cfg.get("shade_threshold", 32))]
     sh(["rocprofv3", "--kernel-trace", "--stats", "--output-format", "csv", "-d", os.path.join(out, "trace"), "--"]
        + quiet, os.path.join(out, "trace.log"), 400)
     print("trace done", flush=True)
