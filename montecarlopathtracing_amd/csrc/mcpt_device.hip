@@ -646,6 +646,14 @@ __device__ inline void handoff_store(unsigned long long *p, unsigned long long v
 // 88 dequeues/us; sharded per XCD the rate scales with the heads).
 __device__ inline uint32_t xcc_id() { return __builtin_amdgcn_s_getreg((3 << 11) | 20) & 7u; }  // hwreg(HW_REG_XCC_ID, 0, 4)
 
+// Uniforms of a launch kept in LDS (k_render).  80-B camera + 16 + 32 B.
+struct __attribute__((aligned(16))) LdsUniforms {
+  mcpt_camera cam;
+  f4 cc;  // generateRay's 0.5 / tan(arg / 2) and W / H (cam_const)
+  f4 root_min, root_max;
+};
+static_assert(sizeof(LdsUniforms) == 128, "LDS uniforms");
+
 struct RenderArgs {
   mcpt_camera cam;
   SceneView S;
@@ -720,14 +728,25 @@ __global__ void __launch_bounds__(64, MCPT_WAVES_PER_SIMD) k_render(RenderArgs A
   const SceneView &S = A.S;
   const int stack_cap = WIN ? kStackWindow + A.spill_stride : A.stack_depth;  // entries (MCPT_DEBUG bound)
   (void)stack_cap;
-  // material table copied to LDS behind the stack (small tables only)
+  // LDS behind the stack: the per-launch uniforms that only segment and frame
+  // starts read (camera, generateRay constants, root box: kept out of the
+  // SGPRs, the scarce register file of this kernel), then the material table
+  // (small tables only)
+  LdsUniforms *U = reinterpret_cast<LdsUniforms *>(lds_stack + A.stack_depth * 64);
+  if (lane == 0) {
+    U->cam = A.cam;
+    const CamConst c0 = cam_const(A.cam, (uint32_t)A.W, (uint32_t)A.H);
+    U->cc = (f4){c0.distance, c0.ratio, 0.0f, 0.0f};
+    U->root_min = S.root_min;
+    U->root_max = S.root_max;
+  }
   const mcpt_material *mats = S.mats;
   if (A.lds_mats) {
-    mcpt_material *lm = reinterpret_cast<mcpt_material *>(lds_stack + A.stack_depth * 64);
+    mcpt_material *lm = reinterpret_cast<mcpt_material *>(U + 1);
     for (int k = lane; k < S.n_mats; k += 64) lm[k] = S.mats[k];
-    __syncthreads();
     mats = lm;
   }
+  __syncthreads();
 
   unsigned long long n_seg = 0, n_nodes = 0, n_tests = 0, n_bad = 0;
   unsigned long long w_t = 0, w_l = 0, w_s = 0, n_fb = 0;
@@ -742,12 +761,12 @@ __global__ void __launch_bounds__(64, MCPT_WAVES_PER_SIMD) k_render(RenderArgs A
   int32_t blk = 0;             // frame block of the pixel (the pending entry's block while kPend)
   f4 hist = (f4){0.0f, 0.0f, 0.0f, 0.0f};
   f4 o = hist, d = hist, color = hist;
-  // uniform generateRay constants, moved to scalar registers
-  CamConst cc = cam_const(A.cam, (uint32_t)A.W, (uint32_t)A.H);
-  cc.distance = as_f(__builtin_amdgcn_readfirstlane(as_i(cc.distance)));
-  cc.ratio = as_f(__builtin_amdgcn_readfirstlane(as_i(cc.ratio)));
   auto primary = [&]() {  // no jitter: every frame re-shoots the same primary ray
-    gen_ray_px(A.cam, cc, pxy & 0xFFFFu, pxy >> 16, (uint32_t)A.W, (uint32_t)A.H, o, d);
+    const f4 c4 = U->cc;
+    CamConst cc;
+    cc.distance = c4.x;
+    cc.ratio = c4.y;
+    gen_ray_px(U->cam, cc, pxy & 0xFFFFu, pxy >> 16, (uint32_t)A.W, (uint32_t)A.H, o, d);
     color = (f4){1.0f, 1.0f, 1.0f, 1.0f};
   };
   // path / traversal state (declared with the pixel state below)
@@ -768,7 +787,7 @@ __global__ void __launch_bounds__(64, MCPT_WAVES_PER_SIMD) k_render(RenderArgs A
     t2 = kFltMax;
     ref = LIT;
     sp = 0;
-    if (slab_pass(box_test<LIT>(S.root_min.xyz, S.root_max.xyz, o.xyz, d.xyz, rinv), kTmin))
+    if (slab_pass(box_test<LIT>(U->root_min.xyz, U->root_max.xyz, o.xyz, d.xyz, rinv), kTmin))
       cur = S.root_leaf >= 0 ? ~S.root_leaf : 0;
     else
       cur = kDone;
@@ -1824,8 +1843,8 @@ int mcpt_render_frames(mcpt_ctx *ctx, const mcpt_scene *scene, const mcpt_camera
   const bool quant = scene->near4q && (T.quantized == 1 || (T.quantized == 0 && scene->near4_bytes > kQuantAutoBytes));
   const int kind = noprune ? 1 : (quant ? 2 : 0);
   const size_t pad = (size_t)std::max(0, T.lds_pad);
-  const size_t lds_plain = (size_t)depth_entries * 64 * sizeof(int32_t) + lds_mats + pad;
-  const size_t lds_win = (size_t)kStackWindow * 64 * sizeof(int32_t) + lds_mats + pad;
+  const size_t lds_plain = (size_t)depth_entries * 64 * sizeof(int32_t) + sizeof(LdsUniforms) + lds_mats + pad;
+  const size_t lds_win = (size_t)kStackWindow * 64 * sizeof(int32_t) + sizeof(LdsUniforms) + lds_mats + pad;
   bool win = false;
   int per_cu = 0;
   if (T.stack_window == 1) {  // forced (tests, experiments): the window even when the whole stack fits in it
@@ -1846,7 +1865,7 @@ int mcpt_render_frames(mcpt_ctx *ctx, const mcpt_scene *scene, const mcpt_camera
   }
   const size_t lds = win ? lds_win : lds_plain;
   const void *kfn = kfns[kind][ctx->stats_on][win][pair];
-  A.stack_depth = win ? kStackWindow : depth_entries;  // the material table follows the stack in LDS
+  A.stack_depth = win ? kStackWindow : depth_entries;  // the uniforms and material table follow the stack in LDS
   A.spill_stride = win ? std::max(0, depth_entries - kStackWindow) : 0;
   const int64_t grid = std::max<int64_t>(1, std::min<int64_t>(tiles, (int64_t)std::max(per_cu, 1) * ctx->n_cu));
   const int64_t spill_need = win ? grid * 64 * (int64_t)A.spill_stride : 0;
