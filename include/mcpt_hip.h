@@ -191,6 +191,8 @@ typedef struct mcpt_tuning {
   int32_t lds_pad;          /* extra LDS bytes per workgroup (occupancy
                                experiments; 0)                                    */
   int32_t queues;           /* work queues (1..8; 8: one per XCD)              */
+  int32_t fetch_threshold;  /* lanes of a wave needing a new queue entry before
+                               the wave claims and starts them together (1)    */
   int32_t quantized;        /* EXACT search tree: 0 auto (the 64-B quantized
                                nodes when the 128-B tree exceeds 32 MiB, the
                                GPU's aggregate L2), 1 quantized whenever the

@@ -673,6 +673,7 @@ struct RenderArgs {
   uint32_t n_queues;          // 1..kQueues
   int32_t lds_mats;           // 1: copy the material table to LDS after the stack
   int32_t chunk;              // queue entries a wave claims per atomic (at least)
+  int32_t th_fetch;           // lanes needing an entry before the wave claims
   int32_t *spill;             // WindowStack spill areas, one per resident lane
   int32_t spill_stride;       // entries per lane (stack depth - window)
 };
@@ -815,8 +816,10 @@ __global__ void __launch_bounds__(64, MCPT_WAVES_PER_SIMD) k_render(RenderArgs A
     // ---- fetch: lanes without work take the next queue entries, from the
     // wave's pool of claimed entries; one atomic claims max(chunk, shortfall)
     {
+      // lanes that need an entry start together once th_fetch of them wait
+      // (their state loads then share one wait), or when no lane is busy
       const unsigned long long mn = __ballot(lst == kNeed);
-      if (mn) {
+      if (mn && (__popcll(mn) >= A.th_fetch || !__ballot(lst == kBusy))) {
         const uint32_t n_need = (uint32_t)__popcll(mn);
         const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(mn >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mn, 0));
         uint32_t q = pool + rank, qx = (qs >> 4) & 15u;
@@ -1445,7 +1448,7 @@ int mcpt_get_stats(mcpt_ctx *c, mcpt_stats *out) {
 int mcpt_set_tuning(mcpt_ctx *c, const mcpt_tuning *t) {
   if (!c) return mcpt::fail(MCPT_ERR_ARG, "set_tuning: null ctx");
   if (t && (t->stack_window < 0 || t->stack_window > 2 || t->quantized < 0 || t->quantized > 2 || t->lds_pad < 0 || t->lds_pad > 65536 ||
-            t->queue_chunk > 4096 || t->leaf_threshold > 64 || t->shade_threshold > 64))
+            t->queue_chunk > 4096 || t->leaf_threshold > 64 || t->shade_threshold > 64 || t->fetch_threshold > 64))
     return mcpt::fail(MCPT_ERR_ARG, "set_tuning: value out of range");
   if (t)
     c->tune = *t;
@@ -1818,6 +1821,7 @@ int mcpt_render_frames(mcpt_ctx *ctx, const mcpt_scene *scene, const mcpt_camera
   A.th_leaf = T.leaf_threshold > 0 ? T.leaf_threshold : (pair ? 16 : 4);
   A.th_shade = T.shade_threshold > 0 ? T.shade_threshold : 32;
   A.chunk = T.queue_chunk > 0 ? T.queue_chunk : 4;  // queue entries per atomic (at least)
+  A.th_fetch = T.fetch_threshold > 0 ? T.fetch_threshold : 1;
   A.n_queues = T.queues > 0 ? (uint32_t)std::min(T.queues, kQueues) : (uint32_t)kQueues;
   const int64_t tiles = (int64_t)A.tiles_x * ((A.local_rows + 7) / 8);
   const int depth_entries = p->mode == MCPT_MODE_NOPRUNE ? scene->stack_depth : scene->stack_depth4;

@@ -192,16 +192,18 @@ class Renderer:
         in scene.schedule.  Both schedules give bit-identical images, so this
         only moves speed.  Returns (schedule, {schedule: best ms})."""
         sched, _, best = self.tune(scene, camera, state, max_depth, max_attempt, frames, trials, shade_thresholds=None,
-                                   **kw)
+                                   fetch_thresholds=None, **kw)
         return sched, {k[0]: v for k, v in best.items()}
 
     def tune(self, scene, camera, state, max_depth, max_attempt, frames=64, trials=1, shade_thresholds=(32, 40, 48),
-             **kw):
-        """tune_schedule over the leaf-test schedule AND the S-phase threshold
-        (mcpt_tuning.shade_threshold; the best differs by scene: veach_mis 48,
-        cbox 40, the 10 M-triangle soup 32).  Every combination gives the same
-        bits.  The winner goes to scene.schedule and the renderer's tuning.
-        Returns (schedule, shade_threshold, {(schedule, threshold): best ms})."""
+             fetch_thresholds=(1, 8), **kw):
+        """tune_schedule over the leaf-test schedule, the S-phase threshold
+        (mcpt_tuning.shade_threshold) and then the fetch threshold
+        (mcpt_tuning.fetch_threshold): their best values differ by scene
+        (veach_mis: S 48, fetch 8; cbox: 40, 8; the 10 M-triangle soup: 32, 1).
+        Every combination gives the same bits.  The winner goes to
+        scene.schedule and the renderer's tuning.  Returns (schedule,
+        shade_threshold, {(schedule, shade, fetch): best ms})."""
         if getattr(self, "_stats_on", False):
             raise L.MCPTError("tune: counters must be off (they change the kernel)")
         base = self.get_tuning()
@@ -209,23 +211,33 @@ class Renderer:
         scratch = ImageState.__new__(ImageState)
         scratch.width, scratch.height, scratch.frames_done = state.width, state.height, state.frames_done
         best = {}
+
+        def trial(sched, th, fe):
+            self.set_tuning(**dict(base, shade_threshold=th, fetch_threshold=fe))
+            scratch.seeds, scratch.hist, scratch.count = state.seeds.clone(), state.hist.clone(), state.count.clone()
+            self.render_frames(scene, camera, scratch, max_depth, max_attempt, frames,
+                               frame_begin=state.frames_done, schedule=sched, **kw)
+            ms = self.stats()["kernel_ms"]
+            best[(sched, th, fe)] = min(best.get((sched, th, fe), ms), ms)
+
+        fe0 = base["fetch_threshold"] or 1  # 0 = the default, 1
         try:
             for _ in range(int(trials)):
                 for th in ths:
-                    self.set_tuning(**dict(base, shade_threshold=th))
                     for sched in (L.SCHED_SINGLE, L.SCHED_PAIRED):
-                        scratch.seeds, scratch.hist, scratch.count = (state.seeds.clone(), state.hist.clone(),
-                                                                      state.count.clone())
-                        self.render_frames(scene, camera, scratch, max_depth, max_attempt, frames,
-                                           frame_begin=state.frames_done, schedule=sched, **kw)
-                        ms = self.stats()["kernel_ms"]
-                        best[(sched, th)] = min(best.get((sched, th), ms), ms)
+                        trial(sched, th, fe0)
+            sched, th, fe = min(best, key=lambda k: (best[k], k))
+            if shade_thresholds and fetch_thresholds:  # then the fetch threshold, with that pair
+                for _ in range(int(trials)):
+                    for f in fetch_thresholds:
+                        if f != fe0:
+                            trial(sched, th, f)
+                sched, th, fe = min(best, key=lambda k: (best[k], k))
         finally:
             self.set_tuning(**base)
-        sched, th = min(best, key=lambda k: (best[k], k))
         scene.schedule = sched
         if shade_thresholds:
-            self.set_tuning(**dict(base, shade_threshold=th))
+            self.set_tuning(**dict(base, shade_threshold=th, fetch_threshold=fe))
         return sched, th, best
 
     # ------------------------------------------------ wavefront (drop-in)
