@@ -294,6 +294,12 @@ int mcpt_state_create(mcpt_ctx *ctx, int32_t width, int32_t height, const uint32
 int mcpt_state_buffers(mcpt_state *st, uint32_t **seeds_dev, float **hist_dev, int32_t **count_dev);
 int mcpt_download(mcpt_ctx *ctx, const mcpt_state *st, float *hist_rgba, int32_t *count, uint32_t *seeds,
                   void *stream);
+/* Checkpoint / resume: mcpt_upload writes host arrays (NULL skips one) into
+ * the state, ordered on `stream` before later renders; a state saved with
+ * mcpt_download and uploaded into a fresh one continues the render exactly
+ * (the per-pixel seed chain, mean and count are the whole of it). */
+int mcpt_upload(mcpt_ctx *ctx, mcpt_state *st, const float *hist_rgba, const int32_t *count, const uint32_t *seeds,
+                void *stream);
 int mcpt_state_destroy(mcpt_state *st);
 
 /* Wavefront kernels on the reference's AoS records, one per reference

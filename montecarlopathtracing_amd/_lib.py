@@ -97,6 +97,7 @@ SIGNATURES = {
     "mcpt_state_create": (_I32, [_P, _I32, _I32, _P, _P]),
     "mcpt_state_buffers": (_I32, [_P, _P, _P, _P]),
     "mcpt_download": (_I32, [_P, _P, _P, _P, _P, _P]),
+    "mcpt_upload": (_I32, [_P, _P, _P, _P, _P, _P]),
     "mcpt_state_destroy": (_I32, [_P]),
     "mcpt_set_stats": (_I32, [_P, _I32]),
     "mcpt_get_stats": (_I32, [_P, _P]),

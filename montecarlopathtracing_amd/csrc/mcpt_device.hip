@@ -1502,6 +1502,19 @@ int mcpt_download(mcpt_ctx *c, const mcpt_state *s, float *hist, int32_t *count,
   return MCPT_OK;
 }
 
+int mcpt_upload(mcpt_ctx *c, mcpt_state *s, const float *hist, const int32_t *count, const uint32_t *seeds,
+                void *stream) {
+  if (!c || !s || s->device != c->device) return mcpt::fail(MCPT_ERR_ARG, "upload: bad argument");
+  HIP_OK(hipSetDevice(c->device));
+  hipStream_t st = (hipStream_t)stream;
+  const size_t n = (size_t)s->width * s->height;
+  if (hist) HIP_OK(hipMemcpyAsync(s->hist, hist, n * 16, hipMemcpyHostToDevice, st));
+  if (count) HIP_OK(hipMemcpyAsync(s->count, count, n * 4, hipMemcpyHostToDevice, st));
+  if (seeds) HIP_OK(hipMemcpyAsync(s->seeds, seeds, n * 4, hipMemcpyHostToDevice, st));
+  HIP_OK(hipStreamSynchronize(st));  // the host arrays may be reused on return
+  return MCPT_OK;
+}
+
 int mcpt_state_destroy(mcpt_state *s) {
   if (!s) return MCPT_OK;
   (void)hipSetDevice(s->device);

@@ -6,6 +6,7 @@
 // infrastructure (tests/test_gpu_abi_host.py drives it).
 //
 //   abi_host <config.json> <configid> <seeds.u32|-> <out_dir> [--frames-per-update F] [--updates U]
+//            [--resume-at K]   (before update K: mcpt_download, a new state, mcpt_upload)
 //
 // init: Config::CONFIG (config.cpp:70-124, '#' comments), loadObject
 // (thirdpartywrapper.cpp:25-99), SceneCL packing + HLBVH<CPU>
@@ -231,6 +232,21 @@ struct App {
     }
   }
 
+  // checkpoint / resume: the image state saved to host arrays, the state
+  // destroyed, a new one created and the saved arrays uploaded into it
+  void checkpoint_resume() {
+    const size_t n = (size_t)width * height;
+    std::vector<float> hist(n * 4);
+    std::vector<int32_t> count(n);
+    std::vector<uint32_t> seeds(n);
+    OK(mcpt_download(ctx, state, hist.data(), count.data(), seeds.data(), nullptr));
+    OK(mcpt_state_destroy(state));
+    state = nullptr;
+    std::vector<uint32_t> zero(n, 0u);
+    OK(mcpt_state_create(ctx, width, height, zero.data(), &state));
+    OK(mcpt_upload(ctx, state, hist.data(), count.data(), seeds.data(), nullptr));
+  }
+
   void save_state(const std::string &path) {
     const size_t n = (size_t)width * height;
     std::vector<float> hist(n * 4);
@@ -261,10 +277,11 @@ int main(int argc, char **argv) {
   try {
     const std::string cfg_path = argv[1];
     const int configid = std::atoi(argv[2]);
-    int fpu = 1, updates = -1;
+    int fpu = 1, updates = -1, resume_at = -1;
     for (int k = 5; k + 1 < argc; k += 2) {
       if (!std::strcmp(argv[k], "--frames-per-update")) fpu = std::atoi(argv[k + 1]);
       else if (!std::strcmp(argv[k], "--updates")) updates = std::atoi(argv[k + 1]);
+      else if (!std::strcmp(argv[k], "--resume-at")) resume_at = std::atoi(argv[k + 1]);
     }
     const std::string text = slurp(cfg_path);
     Parser ps{text};
@@ -286,7 +303,10 @@ int main(int argc, char **argv) {
     app.update(fpu);  // the first update outside the clock (lazy allocations)
     OK(mcpt_get_stats(app.ctx, &st));
     const auto t0 = std::chrono::steady_clock::now();
-    for (int k = 1; k < updates; ++k) app.update(fpu);
+    for (int k = 1; k < updates; ++k) {
+      if (k == resume_at) app.checkpoint_resume();
+      app.update(fpu);
+    }
     OK(mcpt_get_stats(app.ctx, &st));  // waits for the last update
     const double s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
     app.save_state(app.out_dir + "/state.bin");

@@ -95,3 +95,19 @@ def test_cpp_host_batched_updates_equal_single_frames(tmp_path):
     hb, cb, sb = _state(b, w, h)
     assert ha.tobytes() == hb.tobytes() and np.array_equal(ca, cb) and np.array_equal(sa, sb)
     assert int(ca.max()) <= 16  # MAX_ATTEMPT caps the count
+
+
+@needs_exe
+def test_cpp_host_checkpoint_resume_bitexact(tmp_path):
+    """Checkpoint / resume through the C ABI alone: before update 7 the host
+    saves the image state (mcpt_download), destroys it, creates a new one and
+    restores the saved arrays (mcpt_upload); the render continues to the C1
+    golden image bit for bit."""
+    g = gold("image_c1_cbox.npz")
+    w, h, depth, frames, att = (int(x) for x in g["meta"])
+    out = _run(tmp_path, 2, g["seeds_in"], "--updates", frames, "--resume-at", 7)
+    assert out["frames_done"] == frames
+    hist, count, seeds = _state(tmp_path, w, h)
+    assert np.array_equal(count, g["count"])
+    assert np.array_equal(seeds, g["seeds"])
+    assert hist.tobytes() == np.ascontiguousarray(g["hist"], np.float32).tobytes()

@@ -294,6 +294,34 @@ def test_exact_equals_noprune_full_size(rnd):
     dsc.close()
 
 
+def test_launch_knobs_change_no_bits_full_size(rnd):
+    """Size-independent property at a C2-like configuration: every launch-plan
+    knob Renderer.tune and bench.py set (S-phase and fetch thresholds, leaf
+    threshold, queue chunk, block sizing, queue count) moves only speed: the
+    image, counts and seed chains are identical for each setting."""
+    data, cam = scenes.cbox_diffuse(), S.parse_camera(scenes.CBOX_CAM)
+    w = h = 256
+    seeds = R.default_seeds(w * h)
+    dsc = rnd.upload(data)
+    settings = [{}, {"shade_threshold": 48, "fetch_threshold": 8}, {"shade_threshold": 24, "leaf_threshold": 8},
+                {"fetch_threshold": 64, "queue_chunk": 16}, {"block_entries": 4, "max_block_frames": 2},
+                {"queues": 1}, {"queues": 3, "fetch_threshold": 5}]
+    outs = []
+    try:
+        for t in settings:
+            rnd.set_tuning(**t)
+            st = rnd.new_state(w, h, seeds)
+            rnd.render_frames(dsc, cam, st, 8, 1 << 20, 6)
+            torch.cuda.synchronize()
+            outs.append((st.hist.cpu().numpy(), st.count.cpu().numpy(), st.seeds_np()))
+    finally:
+        rnd.set_tuning()
+    for t, o in zip(settings[1:], outs[1:]):
+        for a, b, what in zip(outs[0], o, ("hist", "count", "seeds")):
+            assert_bits_equal(a, b, "%s %s" % (what, t))
+    dsc.close()
+
+
 def test_frame_blocks_handoff_full_size(rnd):
     """Frame blocks of one pixel run on different lanes (and XCDs) within one
     launch, handing the state through memory: any block size gives the same
