@@ -30,6 +30,8 @@ def child(a):
     rnd = R.Renderer(0)
     dsc = rnd.upload(data)
     dsc.schedule = L.SCHED_PAIRED if a.schedule == "paired" else L.SCHED_SINGLE
+    if a.tuning:
+        rnd.set_tuning(**{k: int(v) for k, v in (x.split("=") for x in a.tuning.split(","))})
     st = rnd.new_state(wl["w"], wl["h"])
     rnd.render_frames(dsc, cam, st, wl["depth"], 1 << 30, 4, frames_per_launch=a.fpl)
     ms = []
@@ -48,6 +50,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--schedule", default="paired", choices=["single", "paired"])
+    ap.add_argument("--tuning", default="", help="set_tuning knobs for every library, e.g. shade_threshold=40,fetch_threshold=8")
     ap.add_argument("--child", action="store_true")
     a = ap.parse_args()
     if a.child:
@@ -59,7 +62,7 @@ def main():
             env = dict(os.environ, MCPT_LIB_OVERRIDE=os.path.abspath(lib))
             out = subprocess.run([sys.executable, os.path.abspath(__file__), "--child", "--libs", lib,
                                   "--workload", a.workload, "--frames", str(a.frames), "--fpl", str(a.fpl),
-                                  "--schedule", a.schedule,
+                                  "--schedule", a.schedule, "--tuning", a.tuning,
                                   "--reps", str(a.reps)], env=env, capture_output=True, text=True, timeout=600)
             line = [x for x in out.stdout.splitlines() if x.startswith("AB_RESULT ")]
             if out.returncode != 0 or not line:
