@@ -203,6 +203,14 @@ def summarize(tag):
         # vector-memory address (TA) and data-return (TD) units: busy cycles per CU per kernel cycle
         "ta_busy": round(ctr.get("TA_TA_BUSY_sum", float("nan")) / (N_CU * cycles), 4),
         "td_busy": round(ctr.get("TD_TD_BUSY_sum", float("nan")) / (N_CU * cycles), 4),
+        # the bench line's roofline recomputed with THIS run's counters (the bench
+        # line itself ran before them and carries the previous pmc_summary.json)
+        "roofline_this_run": {
+            "traffic": rd + wr, "avg_launch_ms": r.get("avg_launch_ms"),
+            "achieved": round((rd + wr) / (r["avg_launch_ms"] / 1e3) / 1e9, 2) if r.get("avg_launch_ms") else None,
+            "frac": round((rd + wr) / (r["avg_launch_ms"] / 1e3) / 1e9 / HBM_PEAK_GBS, 5) if r.get("avg_launch_ms") else None,
+            "issue_frac": round(ctr["SQ_ACTIVE_INST_VALU"] / (N_CU * cycles), 4),
+            "td_busy": round(ctr.get("TD_TD_BUSY_sum", float("nan")) / (N_CU * cycles), 4)},
         "counters_timed_dispatch": ctr,
         "sources": ["profiles/%s_%s.csv" % (tag, x) for x in
                     ["kernel_stats", "kernel_trace"] + ["pmc_" + n for n in PASSES] + ["calib_fetch", "calib_write"]],
