@@ -168,7 +168,11 @@ typedef struct mcpt_stats {
                                        reached whose exact box the ray misses */
   int32_t  quantized;               /* 1: the last call searched the 64-B
                                        quantized tree (EXACT mode)            */
-  int32_t  pad1;
+  int32_t  primary_cache;           /* 0: the last call traced every frame's
+                                       primary ray; 1: it read the cached
+                                       primary hits; 2: it computed them too  */
+  double   primary_ms;              /* primary_cache 2: device time of the
+                                       primary-hit pass (part of kernel_ms)   */
 } mcpt_stats;
 
 /* Launch-plan knobs of the fused kernel (speed only: every setting gives the
@@ -197,6 +201,13 @@ typedef struct mcpt_tuning {
                                nodes when the 128-B tree exceeds 32 MiB, the
                                GPU's aggregate L2), 1 quantized whenever the
                                scene has them, 2 the 128-B nodes                 */
+  int32_t primary_cache;    /* every frame re-shoots the same primary ray, so its
+                               hit is computed once per (scene, camera, image,
+                               stripes, mode) and kept in the context: 0 auto
+                               (a call of >= 2 frames, or a one-frame call of
+                               the previous call's view, computes it; every
+                               call with a matching one reads it), 1 always,
+                               2 never                                          */
 } mcpt_tuning;
 
 /* ------------------------------------------------------- version / errors */
@@ -281,6 +292,9 @@ int mcpt_render_frames(mcpt_ctx *ctx, const mcpt_scene *scene, const mcpt_camera
 /* Launch-plan knobs (speed only), kept in the context; NULL resets them.  */
 int mcpt_set_tuning(mcpt_ctx *ctx, const mcpt_tuning *tuning);
 int mcpt_get_tuning(mcpt_ctx *ctx, mcpt_tuning *out);
+/* Forget the primary-hit cache (mcpt_tuning.primary_cache): the next render
+ * call traces or recomputes its primary hits itself (bench.py's timed call). */
+int mcpt_drop_caches(mcpt_ctx *ctx);
 
 /* Per-image state in HBM for C/C++ hosts that do not manage device memory
  * themselves: the reference's randBuffer (scenebuild.cpp:113-120),
@@ -317,6 +331,12 @@ int mcpt_shade(mcpt_ctx *ctx, const mcpt_scene *scene, mcpt_ray *rays_dev,
 /* history.cl func (-D MAX_ATTEMPT): running mean of non-zero samples      */
 int mcpt_accumulate(mcpt_ctx *ctx, float *color_dev, float *hist_dev, int32_t *count_dev,
                     int64_t n, int32_t max_attempt, void *stream);
+/* testkernel.cl func, ColorOut's display pass (colorout.cpp:58-70): per
+ * pixel (pow(r, 1/2.2f), pow(g, 1/2.2f), pow(b, 1/2.2f), 0) into a float4
+ * buffer (the reference writes it to its RGBA32F GL texture).  The reference
+ * shows the current frame's colours before MAX_ATTEMPT and frameBuffer (the
+ * running mean, mcpt_state's hist) after.  n = pixels; may run in place.    */
+int mcpt_gamma_preview(mcpt_ctx *ctx, const float *color_dev, float *out_dev, int64_t n, void *stream);
 
 /* Counters of the last render call (segments etc. need stats enabled);
  * waits for that call's work to finish.                                   */

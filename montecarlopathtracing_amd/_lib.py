@@ -49,14 +49,15 @@ class Stats(ctypes.Structure):
                 ("wave_iterations", ctypes.c_uint64), ("lane_waiting", ctypes.c_uint64), ("lane_idle", ctypes.c_uint64),
                 ("stack_window", ctypes.c_int32), ("workgroups", ctypes.c_int32),
                 ("debug_violations", ctypes.c_uint64), ("phase_ticks", ctypes.c_uint64 * 4),
-                ("leaf_rejects", ctypes.c_uint64), ("quantized", ctypes.c_int32), ("pad1", ctypes.c_int32)]
+                ("leaf_rejects", ctypes.c_uint64), ("quantized", ctypes.c_int32), ("primary_cache", ctypes.c_int32),
+                ("primary_ms", ctypes.c_double)]
 
 
 class Tuning(ctypes.Structure):
     """mcpt_tuning: launch-plan knobs of k_render (speed only; 0 = default)."""
     _fields_ = [(n, ctypes.c_int32) for n in (
         "leaf_threshold", "shade_threshold", "queue_chunk", "block_entries", "max_block_frames", "stack_window",
-        "lds_pad", "queues", "fetch_threshold", "quantized")]
+        "lds_pad", "queues", "fetch_threshold", "quantized", "primary_cache")]
 
 
 class MCPTError(RuntimeError):
@@ -92,8 +93,10 @@ SIGNATURES = {
     "mcpt_intersect": (_I32, [_P, _P, _P, _I64, _P, _F32, _I32, _P]),
     "mcpt_shade": (_I32, [_P, _P, _P, _P, _P, _P, _I64, _I32, _P]),
     "mcpt_accumulate": (_I32, [_P, _P, _P, _P, _I64, _I32, _P]),
+    "mcpt_gamma_preview": (_I32, [_P, _P, _P, _I64, _P]),
     "mcpt_set_tuning": (_I32, [_P, _P]),
     "mcpt_get_tuning": (_I32, [_P, _P]),
+    "mcpt_drop_caches": (_I32, [_P]),
     "mcpt_state_create": (_I32, [_P, _I32, _I32, _P, _P]),
     "mcpt_state_buffers": (_I32, [_P, _P, _P, _P]),
     "mcpt_download": (_I32, [_P, _P, _P, _P, _P, _P]),

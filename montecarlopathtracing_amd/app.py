@@ -96,3 +96,12 @@ class App:
 
     def image(self):
         return self.state.image()
+
+    def preview(self):
+        """ColorOut's display pass (testkernel.cl func, colorout.cpp:69-70 once
+        the history is complete): the running mean gamma-2.2 encoded, H x W x 4
+        floats (w = 0), as the reference writes to its RGBA32F texture."""
+        if not self._init:
+            self.init()
+        out = self.renderer.gamma_preview(self.state.hist)
+        return out.cpu().numpy().reshape(self.h, self.w, 4)

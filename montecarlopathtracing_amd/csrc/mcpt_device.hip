@@ -19,6 +19,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <climits>
 #include <cstdio>
 #include <cstdlib>
@@ -126,6 +127,7 @@ struct SceneView {
 
 struct mcpt_scene {
   int device;
+  uint64_t uid = 0;  // never reused: keys the context's primary-hit cache
   DevNode4 *near4 = nullptr;
   DevNode4 *nodes4 = nullptr;
   int32_t stack_depth4 = 1;  // EXACT: max of both 4-wide trees' stack needs
@@ -179,6 +181,25 @@ constexpr bool kDebug = false;
 #define MCPT_DCHECK(cond, slot) true
 #endif
 
+// The primary hit of a pixel (k_primary): the reference re-shoots the same
+// primary ray every frame (rayGenerator.cl has no jitter), so its closest hit
+// is the same in every frame; k_render reads it instead of tracing segment 0.
+// nrm = the hit triangle's packed normal (material id bits in .w), t = the
+// closest-hit distance (kFltMax: miss).
+struct __attribute__((aligned(16))) PrimHit {
+  f4 nrm;
+  float t;
+  int32_t pad[3];
+};
+static_assert(sizeof(PrimHit) == 32, "32-B primary hit");
+// What a primary-hit cache was computed for: same scene, camera, image,
+// stripes and mode give the same hits.
+struct PrimKey {
+  uint64_t scene_uid;
+  mcpt_camera cam;
+  int32_t w, h, stripe_rows, stripe_index, stripe_count, mode;
+};
+
 struct mcpt_ctx {
   int device;
   int n_cu = 0;
@@ -202,6 +223,13 @@ struct mcpt_ctx {
   bool last_pending = false;              // the last render call's events/counters not read yet
   bool last_stats = false;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  hipEvent_t ev_prim = nullptr;           // after k_primary, when the call ran it
+  PrimHit *d_prim = nullptr;              // primary-hit cache, one record per pixel
+  int64_t prim_cap = 0;                   // pixels
+  bool prim_valid = false;
+  PrimKey prim_key;                       // what d_prim holds
+  bool seen_valid = false;
+  PrimKey seen_key;                       // the previous render call's view
 };
 
 struct mcpt_state {
@@ -676,6 +704,7 @@ struct RenderArgs {
   int32_t th_fetch;           // lanes needing an entry before the wave claims
   int32_t *spill;             // WindowStack spill areas, one per resident lane
   int32_t spill_stride;       // entries per lane (stack depth - window)
+  const PrimHit *prim;        // per-pixel primary hits (k_primary), nullptr: trace segment 0
 };
 
 __device__ inline int32_t global_row(int32_t lr, const RenderArgs &A) {
@@ -793,6 +822,21 @@ __global__ void __launch_bounds__(64, MCPT_WAVES_PER_SIMD) k_render(RenderArgs A
     else
       cur = kDone;
   };
+  // a frame's first segment: the primary ray's hit is the same every frame
+  // (k_primary computed it once), so the lane goes straight to S with it
+  auto begin_frame = [&]() {
+    if (A.prim) {
+      const PrimHit *ph = A.prim + ((size_t)(pxy >> 16) * (size_t)A.W + (pxy & 0xFFFFu));
+      best_nrm = ph->nrm;
+      best_t = ph->t;
+      t2 = kFltMax;
+      ref = LIT;
+      sp = 0;
+      cur = kDone;
+    } else {
+      begin_segment();
+    }
+  };
   // Queue entry q of queue x = block * items + slot: frame block q / items of
   // pixel slot q % items of that queue's tiles.  Blocks of one pixel run in
   // order: the lane that takes (p, b > 0) waits until the lane that ran
@@ -898,7 +942,7 @@ __global__ void __launch_bounds__(64, MCPT_WAVES_PER_SIMD) k_render(RenderArgs A
           lst = kBusy;
           f = 0;
           primary();
-          begin_segment();
+          begin_frame();
         }
       }
     }
@@ -1073,7 +1117,7 @@ __global__ void __launch_bounds__(64, MCPT_WAVES_PER_SIMD) k_render(RenderArgs A
         cur = S.root_leaf >= 0 ? ~S.root_leaf : 0;  // the root box passed: there were hits
       } else if (in_s) {
         if (STATS) n_seg++;
-        bool done;
+        bool done, fresh = false;
         if (best_t >= kFltMax) {  // shade.cl:92-96 — miss: black, terminate
           color = (f4){0.0f, 0.0f, 0.0f, 0.0f};
           done = true;
@@ -1099,7 +1143,10 @@ __global__ void __launch_bounds__(64, MCPT_WAVES_PER_SIMD) k_render(RenderArgs A
           if (A.frame_begin + f0 + f <= A.max_attempt) (void)accumulate_one(color, hist, cnt, A.max_attempt);
           ++f;
           const int32_t fend = min(A.fpl, A.frames - f0);
-          if (f < fend) primary();
+          if (f < fend) {
+            primary();
+            fresh = true;
+          }
           if (f == fend) {  // block complete: write back, fetch another next iteration
             const int32_t pid = (int32_t)(pxy >> 16) * A.W + (int32_t)(pxy & 0xFFFFu);
             if (blk + 1 < A.blocks) {  // publish for the lane that takes the next block
@@ -1119,7 +1166,12 @@ __global__ void __launch_bounds__(64, MCPT_WAVES_PER_SIMD) k_render(RenderArgs A
             lst = kNeed;
           }
         }
-        if (lst == kBusy) begin_segment();
+        if (lst == kBusy) {
+          if (fresh)
+            begin_frame();
+          else
+            begin_segment();
+        }
       }
     }
     MCPT_TICK(3);
@@ -1190,6 +1242,32 @@ __global__ void __launch_bounds__(64) k_intersect(SceneView S, const mcpt_ray *r
   hits[id] = h;
 }
 
+// The primary hit of every pixel of this rank's stripes (the cache k_render
+// reads at each frame start, PrimHit): the frame's first ray (gen_ray_px, as
+// k_render's frame start makes it) traced with the same traversal k_intersect
+// uses, which is the reference's closest hit (EXACT: the order-free search
+// with its fallback; NOPRUNE: the reference tree itself).
+template <int MODE>
+__global__ void __launch_bounds__(64) k_primary(RenderArgs A, PrimHit *out) {
+  extern __shared__ int32_t lds_stack[];
+  const int64_t i = (int64_t)blockIdx.x * 64 + threadIdx.x;  // local pixel: lr * W + x
+  if (i >= (int64_t)A.local_rows * A.W) return;
+  const int32_t lr = (int32_t)(i / A.W), x = (int32_t)(i - (int64_t)lr * A.W);
+  const int32_t y = global_row(lr, A);
+  f4 o, d;
+  gen_ray_px(A.cam, cam_const(A.cam, (uint32_t)A.W, (uint32_t)A.H), (uint32_t)x, (uint32_t)y, (uint32_t)A.W,
+             (uint32_t)A.H, o, d);
+  uint32_t fallbacks = 0;
+  const Trace tr = MODE == MCPT_MODE_NOPRUNE ? traverse_noprune(A.S, o.xyz, d.xyz, kTmin, lds_stack + threadIdx.x, 64)
+                                             : traverse_exact(A.S, o.xyz, d.xyz, kTmin, lds_stack + threadIdx.x, 64,
+                                                              fallbacks);
+  PrimHit h;
+  h.nrm = tr.tri >= 0 ? A.S.tris[tr.tri].nrm : (f4){0.0f, 0.0f, 0.0f, 0.0f};
+  h.t = tr.t;
+  h.pad[0] = h.pad[1] = h.pad[2] = 0;
+  out[(size_t)y * A.W + x] = h;
+}
+
 __global__ void k_shade(const mcpt_material *mats, mcpt_ray *rays, const mcpt_hit *hits, f4 *colors,
                         uint32_t *seeds, int64_t n, int max_depth) {
   int64_t id = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -1232,6 +1310,19 @@ __global__ void k_accumulate(f4 *colors, f4 *hist, int32_t *count, int64_t n, in
   count[id] = c;
 }
 
+// testkernel.cl func (the GL display of ColorOut::outputColorCL,
+// colorout.cpp:58-70): per pixel (pow(r, 1/2.2f), pow(g, ..), pow(b, ..), 0)
+// into the display's RGBA32F texture (openglapp.cpp:84).  Headless here: the
+// texture is a float4 buffer.  `1/2.2f` is the reference's constant (int 1 /
+// float 2.2f, folded at compile time); pow is OpenCL's, i.e. ocml's.
+__global__ void k_gamma_preview(const f4 *__restrict__ color, f4 *__restrict__ out, int64_t n) {
+  const int64_t id = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (id >= n) return;
+  constexpr float kInvGamma = 1 / 2.2f;
+  const f4 c = color[id];
+  out[id] = (f4){cl_pow(c.x, kInvGamma), cl_pow(c.y, kInvGamma), cl_pow(c.z, kInvGamma), 0.0f};
+}
+
 // =================================================================== ABI
 extern "C" {
 
@@ -1260,7 +1351,8 @@ int mcpt_ctx_create(int32_t device, mcpt_ctx **out) {
   std::memset(&c->tune, 0, sizeof(c->tune));
   if (hipDeviceGetAttribute(&c->n_cu, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess ||
       hipMalloc(&c->d_stats, kStatSlots * sizeof(unsigned long long)) != hipSuccess ||
-      hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess) {
+      hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess ||
+      hipEventCreate(&c->ev_prim) != hipSuccess) {
     delete c;
     return mcpt::fail(MCPT_ERR_HIP, "ctx_create: allocation failed");
   }
@@ -1276,8 +1368,10 @@ int mcpt_ctx_destroy(mcpt_ctx *c) {
   if (c->d_queue) (void)hipFree(c->d_queue);
   if (c->d_handoff) (void)hipFree(c->d_handoff);
   if (c->d_spill) (void)hipFree(c->d_spill);
+  if (c->d_prim) (void)hipFree(c->d_prim);
   if (c->ev0) (void)hipEventDestroy(c->ev0);
   if (c->ev1) (void)hipEventDestroy(c->ev1);
+  if (c->ev_prim) (void)hipEventDestroy(c->ev_prim);
   delete c;
   return MCPT_OK;
 }
@@ -1422,6 +1516,10 @@ int mcpt_get_stats(mcpt_ctx *c, mcpt_stats *out) {
     float ms = 0.0f;
     HIP_OK(hipEventElapsedTime(&ms, c->ev0, c->ev1));
     c->last.kernel_ms = ms;
+    if (c->last.primary_cache == 2) {  // k_primary's share of kernel_ms
+      HIP_OK(hipEventElapsedTime(&ms, c->ev0, c->ev_prim));
+      c->last.primary_ms = ms;
+    }
     if (c->last_stats) {
       unsigned long long h[kStatSlots];
       HIP_OK(hipMemcpy(h, c->d_stats, sizeof(h), hipMemcpyDeviceToHost));
@@ -1447,13 +1545,21 @@ int mcpt_get_stats(mcpt_ctx *c, mcpt_stats *out) {
 
 int mcpt_set_tuning(mcpt_ctx *c, const mcpt_tuning *t) {
   if (!c) return mcpt::fail(MCPT_ERR_ARG, "set_tuning: null ctx");
-  if (t && (t->stack_window < 0 || t->stack_window > 2 || t->quantized < 0 || t->quantized > 2 || t->lds_pad < 0 || t->lds_pad > 65536 ||
+  if (t && (t->stack_window < 0 || t->stack_window > 2 || t->quantized < 0 || t->quantized > 2 ||
+            t->primary_cache < 0 || t->primary_cache > 2 || t->lds_pad < 0 || t->lds_pad > 65536 ||
             t->queue_chunk > 4096 || t->leaf_threshold > 64 || t->shade_threshold > 64 || t->fetch_threshold > 64))
     return mcpt::fail(MCPT_ERR_ARG, "set_tuning: value out of range");
   if (t)
     c->tune = *t;
   else
     std::memset(&c->tune, 0, sizeof(c->tune));
+  return MCPT_OK;
+}
+
+int mcpt_drop_caches(mcpt_ctx *c) {
+  if (!c) return mcpt::fail(MCPT_ERR_ARG, "drop_caches: null ctx");
+  c->prim_valid = false;
+  c->seen_valid = false;
   return MCPT_OK;
 }
 
@@ -1706,7 +1812,9 @@ int mcpt_scene_upload(mcpt_ctx *ctx, const mcpt_triangle *tris, int64_t n_tris, 
   float diag = std::sqrt(dx * dx + dy * dy + dz * dz);
 
   HIP_OK(hipSetDevice(ctx->device));
+  static std::atomic<uint64_t> scene_uids{0};
   mcpt_scene *s = new mcpt_scene();
+  s->uid = ++scene_uids;
   s->device = ctx->device;
   if (hipMalloc(&s->near4, near.size() * sizeof(DevNode4)) != hipSuccess ||
       hipMalloc(&s->nodes4, dn4.size() * sizeof(DevNode4)) != hipSuccess ||
@@ -1959,6 +2067,55 @@ int mcpt_render_frames(mcpt_ctx *ctx, const mcpt_scene *scene, const mcpt_camera
   if (ctx->stats_on || kDebug || kTiming)
     HIP_OK(hipMemsetAsync(ctx->d_stats, 0, kStatSlots * sizeof(unsigned long long), st));
   HIP_OK(hipEventRecord(ctx->ev0, st));
+  // primary-hit cache (PrimHit): computed once per (scene, camera, image,
+  // stripes, mode) and kept across calls; auto (0) computes it for a call of
+  // two or more frames, or for a one-frame call of the same view as the
+  // previous call (the reference's one frame per update()); 1 always, 2
+  // never.  Speed only: the same bits either way.
+  A.prim = nullptr;
+  int prim_state = 0;
+  if (T.primary_cache != 2 && tiles > 0 && p->frames > 0) {
+    PrimKey key;
+    std::memset(&key, 0, sizeof key);
+    key.scene_uid = scene->uid;
+    std::memcpy(&key.cam, cam, sizeof key.cam);
+    key.w = p->width;
+    key.h = p->height;
+    key.stripe_rows = p->stripe_rows;
+    key.stripe_index = p->stripe_index;
+    key.stripe_count = p->stripe_count;
+    key.mode = p->mode;
+    const bool have = ctx->prim_valid && std::memcmp(&key, &ctx->prim_key, sizeof key) == 0;
+    const bool again = ctx->seen_valid && std::memcmp(&key, &ctx->seen_key, sizeof key) == 0;
+    ctx->seen_key = key;
+    ctx->seen_valid = true;
+    if (have || T.primary_cache == 1 || p->frames >= 2 || again) {
+      if (!have) {
+        const int64_t n_px = (int64_t)p->width * p->height;
+        if (n_px > ctx->prim_cap) {
+          ctx->prim_valid = false;
+          if (ctx->d_prim) HIP_OK(hipFree(ctx->d_prim));
+          ctx->d_prim = nullptr;
+          ctx->prim_cap = 0;
+          HIP_OK(hipMalloc(&ctx->d_prim, (size_t)n_px * sizeof(PrimHit)));
+          ctx->prim_cap = n_px;
+        }
+        const int64_t n_loc = (int64_t)A.local_rows * p->width;
+        const size_t lds_p = (size_t)depth_entries * 64 * sizeof(int32_t);
+        const dim3 g((unsigned)((n_loc + 63) / 64));
+        if (noprune)
+          hipLaunchKernelGGL(k_primary<MCPT_MODE_NOPRUNE>, g, dim3(64), lds_p, st, A, ctx->d_prim);
+        else
+          hipLaunchKernelGGL(k_primary<MCPT_MODE_EXACT>, g, dim3(64), lds_p, st, A, ctx->d_prim);
+        HIP_OK(hipGetLastError());
+        HIP_OK(hipEventRecord(ctx->ev_prim, st));
+        ctx->prim_key = key;
+        ctx->prim_valid = true;
+      }
+      A.prim = ctx->d_prim;
+      prim_state = have ? 1 : 2;
+    }
+  }
   int launches = 0;
   if (tiles > 0 && p->frames > 0) {
     HIP_OK(hipMemsetAsync(ctx->d_queue, 0, (size_t)n_launch * kQueues * kQueueStride * sizeof(uint32_t), st));
@@ -1988,6 +2145,7 @@ int mcpt_render_frames(mcpt_ctx *ctx, const mcpt_scene *scene, const mcpt_camera
   ctx->last.stack_window = win ? 1 : 0;
   ctx->last.quantized = kind == 2 ? 1 : 0;
   ctx->last.workgroups = (int32_t)grid;
+  ctx->last.primary_cache = prim_state;
   ctx->last_pending = true;
   ctx->last_stats = ctx->stats_on || kDebug || kTiming;
   return MCPT_OK;
@@ -2038,6 +2196,16 @@ int mcpt_accumulate(mcpt_ctx *ctx, float *color, float *hist, int32_t *count, in
   HIP_OK(hipSetDevice(ctx->device));
   hipLaunchKernelGGL(k_accumulate, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream, (f4 *)color,
                      (f4 *)hist, count, n, max_attempt);
+  HIP_OK(hipGetLastError());
+  return MCPT_OK;
+}
+
+int mcpt_gamma_preview(mcpt_ctx *ctx, const float *color, float *out, int64_t n, void *stream) {
+  if (!ctx || !color || !out || n < 0) return mcpt::fail(MCPT_ERR_ARG, "gamma_preview: bad argument");
+  if (n == 0) return MCPT_OK;
+  HIP_OK(hipSetDevice(ctx->device));
+  hipLaunchKernelGGL(k_gamma_preview, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
+                     (const f4 *)color, (f4 *)out, n);
   HIP_OK(hipGetLastError());
   return MCPT_OK;
 }

@@ -134,6 +134,11 @@ class Renderer:
             setattr(t, k, int(v))
         L.check(L.lib().mcpt_set_tuning(self.ctx, ctypes.byref(t)))
 
+    def drop_caches(self):
+        """mcpt_drop_caches: forget the primary-hit cache; the next render call
+        recomputes (or traces) the primary hits itself."""
+        L.check(L.lib().mcpt_drop_caches(self.ctx))
+
     def get_tuning(self):
         t = L.Tuning()
         L.check(L.lib().mcpt_get_tuning(self.ctx, ctypes.byref(t)))
@@ -268,6 +273,18 @@ class Renderer:
         n = count.numel()
         L.check(L.lib().mcpt_accumulate(self.ctx, L.ptr(color), L.ptr(hist), L.ptr(count), n, int(max_attempt),
                                         _stream()))
+
+    def gamma_preview(self, color, out=None):
+        """testkernel.cl func (ColorOut's GL display pass): float4 colours ->
+        (pow(c, 1/2.2f) per channel, w = 0), a new float32 (n, 4) tensor unless
+        `out` is given (may be `color` itself)."""
+        if color.dtype != torch.float32 or not color.is_cuda or color.numel() % 4:
+            raise L.MCPTError("gamma_preview: a float32 CUDA tensor of float4 colours")
+        color = color.contiguous()
+        if out is None:
+            out = torch.empty_like(color)
+        L.check(L.lib().mcpt_gamma_preview(self.ctx, L.ptr(color), L.ptr(out), color.numel() // 4, _stream()))
+        return out.view(-1, 4)
 
 
 def records(buf, dtype):

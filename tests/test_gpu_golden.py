@@ -197,6 +197,56 @@ def test_app_from_config_json_reproduces_c1(tmp_path):
     app.update(1)
     assert app.dumped and os.path.basename(app.dumped) == "cbox.obj.hdr"
     assert open(app.dumped, "rb").read() == S.encode_hdr(app.image())
+    # ColorOut's display pass after the history is complete: frameBuffer, gamma 2.2
+    pv = app.preview()
+    ref = gamma_reference(app.image())
+    assert_within_ulp(pv, ref, 1, "preview")
+
+
+def gamma_reference(c):
+    """testkernel.cl func in float64: pow(c, 1/2.2f) per channel (the float
+    constant), rounded to float32; w = 0."""
+    with np.errstate(invalid="ignore", over="ignore"):
+        out = np.power(c.astype(np.float64), np.float64(np.float32(1) / np.float32(2.2))).astype(np.float32)
+    out[..., 3] = 0.0
+    return out
+
+
+def assert_within_ulp(a, b, ulp, what):
+    a = np.asarray(a, np.float32)
+    b = np.asarray(b, np.float32)
+    nan = np.isnan(b)
+    assert np.array_equal(np.isnan(a), nan), what + ": NaN pattern"
+    ia = a[~nan].view(np.int32).astype(np.int64)
+    ib = b[~nan].view(np.int32).astype(np.int64)
+    d = np.abs(ia - ib)
+    assert np.all(np.sign(a[~nan]) == np.sign(b[~nan])) and d.max(initial=0) <= ulp, \
+        "%s: %d values beyond %d ulp (max %d)" % (what, int((d > ulp).sum()), ulp, int(d.max(initial=0)))
+
+
+def test_gamma_preview_is_opencl_pow(rnd):
+    """testkernel.cl func: pow(c, 1/2.2f) per channel with OpenCL's pow (ocml;
+    the reference kernel writes an RGBA32F GL texture, not runnable headless,
+    so the bar is the correctly rounded value within 1 ulp plus exact special
+    cases), w = 0, in place too."""
+    rng = np.random.default_rng(7)
+    vals = np.concatenate([
+        rng.random(40000, dtype=np.float32),                       # the usual [0, 1) radiance
+        rng.random(20000, dtype=np.float32) * np.float32(100.0),   # lights, over-exposed means
+        np.float32(2.0) ** rng.integers(-149, 127, 4000).astype(np.float32),  # every binade, subnormals
+        np.array([0.0, -0.0, 1.0, np.inf, np.nan, -1.0, -0.5, 1e-45, 3.4e38], np.float32),
+    ]).astype(np.float32)
+    vals = np.concatenate([vals, np.zeros((-len(vals)) % 4, np.float32)])
+    col = vals.reshape(-1, 4)
+    dev = torch.from_numpy(col.copy()).to(rnd.device)
+    out = rnd.gamma_preview(dev).cpu().numpy()
+    ref = gamma_reference(col)
+    assert np.all(out[:, 3] == 0.0) and not np.signbit(out[:, 3]).any()
+    assert_within_ulp(out[:, :3], ref[:, :3], 1, "gamma")
+    sp = out[:, :3].ravel()[np.isin(col[:, :3].ravel(), [0.0, 1.0, np.inf])]
+    assert np.array_equal(sp, np.power(col[:, :3].ravel()[np.isin(col[:, :3].ravel(), [0.0, 1.0, np.inf])], 1.0))
+    rnd.gamma_preview(dev, out=dev)                                # in place
+    assert np.array_equal(dev.cpu().numpy().view(np.int32), out.view(np.int32))
 
 
 def test_cli_runs(tmp_path):

@@ -276,6 +276,60 @@ def test_render_frames_chunked_and_striped_bitexact(rnd):
     dsc.close()
 
 
+@needs_ref
+@pytest.mark.parametrize("mode", [L.MODE_EXACT, L.MODE_NOPRUNE])
+@pytest.mark.parametrize("name,getter,camjson", [("cbox", scenes.cbox, scenes.CBOX_CAM), ("mis", scenes.mis, scenes.MIS_CAM)])
+def test_primary_hit_cache_bitexact(rnd, name, getter, camjson, mode):
+    """Every frame re-shoots the same primary ray (rayGenerator.cl has no
+    jitter), so k_render reads each pixel's primary hit from a cache computed
+    once per (scene, camera, image, stripes, mode).  Off, always, and auto
+    across split calls: the reference's bits every time, and the cache is
+    computed, reused and invalidated when it should be."""
+    data, cam = getter(), S.parse_camera(camjson)
+    w, h, depth, frames, attempt = 48, 40, 6, 5, 8
+    seeds = R.default_seeds(w * h)
+    rh, rc, rs = refgpu.render(data, cam, w, h, depth, frames, attempt, seeds)
+    dsc = rnd.upload(data)
+
+    def check(st, what):
+        torch.cuda.synchronize()
+        assert_bits_equal(st.count.cpu().numpy(), rc, what + "/count")
+        assert_bits_equal(st.seeds_np(), rs, what + "/seeds")
+        assert_bits_equal(st.hist.cpu().numpy(), rh, what + "/hist")
+
+    try:
+        for pc, want in ((2, 0), (1, 2)):
+            rnd.set_tuning(primary_cache=pc)
+            st = rnd.new_state(w, h, seeds)
+            rnd.render_frames(dsc, cam, st, depth, attempt, frames, mode=mode)
+            assert rnd.stats()["primary_cache"] == want
+            check(st, "primary_cache=%d" % pc)
+        rnd.set_tuning()
+        dsc2 = rnd.upload(data)  # a new scene: the cache of dsc no longer applies
+        st = rnd.new_state(w, h, seeds)
+        rnd.render_frames(dsc2, cam, st, depth, attempt, 1, mode=mode)
+        assert rnd.stats()["primary_cache"] == 0  # a one-frame call does not build it
+        rnd.render_frames(dsc2, cam, st, depth, attempt, 2, mode=mode)
+        assert rnd.stats()["primary_cache"] == 2  # built
+        rnd.render_frames(dsc2, cam, st, depth, attempt, 1, mode=mode)
+        assert rnd.stats()["primary_cache"] == 1  # reused, one frame too
+        rnd.render_frames(dsc2, cam, st, depth, attempt, 1, mode=mode)
+        check(st, "auto, split calls")
+        other = cam.copy()
+        other.view(np.float32)[0] += np.float32(0.25)  # another camera
+        st2 = rnd.new_state(w, h, seeds)
+        rnd.render_frames(dsc2, other, st2, depth, attempt, 1, mode=mode)
+        assert rnd.stats()["primary_cache"] == 0  # a new view, one frame: traced
+        rnd.render_frames(dsc2, other, st2, depth, attempt, 1, mode=mode)
+        assert rnd.stats()["primary_cache"] == 2  # the same view again: built
+        rnd.render_frames(dsc2, cam, st2, depth, attempt, 2, mode=mode)
+        assert rnd.stats()["primary_cache"] == 2  # back to the first camera: rebuilt
+        dsc2.close()
+    finally:
+        rnd.set_tuning()
+    dsc.close()
+
+
 def test_exact_equals_noprune_full_size(rnd):
     """Size-independent property at a C2-like configuration: the pruned
     traversal reproduces the exhaustive reference traversal exactly."""
@@ -305,7 +359,7 @@ def test_launch_knobs_change_no_bits_full_size(rnd):
     dsc = rnd.upload(data)
     settings = [{}, {"shade_threshold": 48, "fetch_threshold": 8}, {"shade_threshold": 24, "leaf_threshold": 8},
                 {"fetch_threshold": 64, "queue_chunk": 16}, {"block_entries": 4, "max_block_frames": 2},
-                {"queues": 1}, {"queues": 3, "fetch_threshold": 5}]
+                {"queues": 1}, {"queues": 3, "fetch_threshold": 5}, {"primary_cache": 2}, {"primary_cache": 1}]
     outs = []
     try:
         for t in settings:
