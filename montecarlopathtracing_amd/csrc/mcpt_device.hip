@@ -1250,9 +1250,12 @@ __global__ void __launch_bounds__(64) k_intersect(SceneView S, const mcpt_ray *r
 template <int MODE>
 __global__ void __launch_bounds__(64) k_primary(RenderArgs A, PrimHit *out) {
   extern __shared__ int32_t lds_stack[];
-  const int64_t i = (int64_t)blockIdx.x * 64 + threadIdx.x;  // local pixel: lr * W + x
-  if (i >= (int64_t)A.local_rows * A.W) return;
-  const int32_t lr = (int32_t)(i / A.W), x = (int32_t)(i - (int64_t)lr * A.W);
+  // one 8x8 tile of the rank's rows per wave: neighbouring primary rays walk
+  // the same nodes, so the wave's gathers share lines
+  const int32_t tile = (int32_t)blockIdx.x;
+  const int32_t x = (tile % A.tiles_x) * 8 + (int32_t)(threadIdx.x & 7u);
+  const int32_t lr = (tile / A.tiles_x) * 8 + (int32_t)(threadIdx.x >> 3);
+  if (x >= A.W || lr >= A.local_rows) return;
   const int32_t y = global_row(lr, A);
   f4 o, d;
   gen_ray_px(A.cam, cam_const(A.cam, (uint32_t)A.W, (uint32_t)A.H), (uint32_t)x, (uint32_t)y, (uint32_t)A.W,
@@ -2100,9 +2103,8 @@ int mcpt_render_frames(mcpt_ctx *ctx, const mcpt_scene *scene, const mcpt_camera
           HIP_OK(hipMalloc(&ctx->d_prim, (size_t)n_px * sizeof(PrimHit)));
           ctx->prim_cap = n_px;
         }
-        const int64_t n_loc = (int64_t)A.local_rows * p->width;
         const size_t lds_p = (size_t)depth_entries * 64 * sizeof(int32_t);
-        const dim3 g((unsigned)((n_loc + 63) / 64));
+        const dim3 g((unsigned)tiles);  // 8x8 pixel tiles of this rank's rows
         if (noprune)
           hipLaunchKernelGGL(k_primary<MCPT_MODE_NOPRUNE>, g, dim3(64), lds_p, st, A, ctx->d_prim);
         else
