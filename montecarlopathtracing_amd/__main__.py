@@ -1,7 +1,7 @@
 """Command line: render a reference config.json on the GPU(s) and write the .hdr,
 or, for a "testbvh" / "testall" entry, print the BVH metrics (main.cpp:11-25).
 
-    python -m montecarlopathtracing_amd [config.json] [--configid N] [--out DIR]
+    python -m montecarlopathtracing_amd [config.json] [--configid N] [--out DIR] [--preview PNG]
     torchrun --nproc-per-node 8 -m montecarlopathtracing_amd config.json   (row-stripe tiles)
 """
 import argparse
@@ -16,6 +16,7 @@ def main(argv=None):
     ap.add_argument("--configid", type=int, default=None)
     ap.add_argument("--out", default=".")
     ap.add_argument("--frames", type=int, default=None, help="override attempt+1 frames")
+    ap.add_argument("--preview", default=None, help="also write the gamma-2.2 display image (testkernel.cl) as PNG")
     a = ap.parse_args(argv)
     from . import config as C
     cfg = C.Config(a.config, a.configid)
@@ -35,6 +36,9 @@ def main(argv=None):
     else:
         path = app.run()
     print("wrote %s (%dx%d, %d frames, %.2f s)" % (path, app.w, app.h, app.attempt_count, time.time() - t0))
+    if a.preview:
+        from . import scene as S
+        print("wrote", S.write_png(a.preview, app.preview()))
     return 0
 
 

@@ -90,6 +90,36 @@ def write_hdr(path, rgba, flip=True):
     L.check(L.lib().mcpt_write_hdr(path.encode(), a.shape[1], a.shape[0], L.ptr(a), int(flip)))
 
 
+def preview_rgb8(preview, flip=True):
+    """8-bit RGB of a gamma-encoded preview (mcpt_gamma_preview's float4s):
+    round(clamp(c, 0, 1) * 255) per channel; flip=True puts the image's top
+    row first, as the .hdr dump does (row 0 of the render is its bottom)."""
+    a = np.asarray(preview, np.float32)[..., :3]
+    a = np.nan_to_num(a, nan=0.0, posinf=1.0, neginf=0.0)
+    q = np.floor(np.clip(a, 0.0, 1.0) * np.float32(255.0) + np.float32(0.5)).astype(np.uint8)
+    return np.ascontiguousarray(q[::-1] if flip else q)
+
+
+def write_png(path, preview, flip=True):
+    """The display's gamma-2.2 image as a PNG (the optional
+    preview of testkernel.cl's pass): 8-bit RGB, no interlace, zlib-compressed
+    rows with filter 0."""
+    import struct
+    import zlib
+    q = preview_rgb8(preview, flip)
+    h, w = q.shape[:2]
+    raw = b"".join(b"\x00" + q[y].tobytes() for y in range(h))
+
+    def chunk(tag, data):
+        return struct.pack(">I", len(data)) + tag + data + struct.pack(">I", zlib.crc32(tag + data) & 0xFFFFFFFF)
+
+    png = (b"\x89PNG\r\n\x1a\n" + chunk(b"IHDR", struct.pack(">IIBBBBB", w, h, 8, 2, 0, 0, 0))
+           + chunk(b"IDAT", zlib.compress(raw, 6)) + chunk(b"IEND", b""))
+    with open(path, "wb") as fh:
+        fh.write(png)
+    return path
+
+
 class SceneData:
     """Host-side scene: packed triangles, HLBVH nodes, materials."""
 

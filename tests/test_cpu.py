@@ -549,3 +549,21 @@ def test_lcv_oracle_equals_reference_host():
     w, h = (int(x) for x in g["lcv_size"])
     v, _ = O.bvh_lcv(scenes.cbox().nodes, S.parse_camera(scenes.CBOX_CAM), w, h)
     assert np.float32(v).view(np.uint32) == g["lcv_cbox_bits"]
+
+
+def test_png_preview_round_trip(tmp_path):
+    """The gamma-2.2 display image as PNG (testkernel.cl's pass, SURVEY §8(f)
+    rank 2): 8-bit round(clamp(c, 0, 1) * 255), top row first like the .hdr,
+    decoded back bit for bit."""
+    PIL = pytest.importorskip("PIL.Image")
+    rng = np.random.default_rng(3)
+    pv = rng.uniform(-0.2, 1.3, (37, 53, 4)).astype(np.float32)
+    pv[0, 0, :3] = [np.nan, np.inf, -np.inf]
+    pv[..., 3] = 0.0
+    S.write_png(str(tmp_path / "p.png"), pv)
+    with PIL.open(tmp_path / "p.png") as im:
+        got = np.asarray(im.convert("RGB"))
+    want = np.clip(np.nan_to_num(pv[::-1, :, :3], nan=0.0, posinf=1.0, neginf=0.0), 0, 1)
+    want = np.floor(want * 255 + 0.5).astype(np.uint8)
+    assert got.shape == (37, 53, 3) and np.array_equal(got, want)
+    assert np.array_equal(got[-1, 0], [0, 255, 0])  # NaN -> 0, +inf -> 1, -inf -> 0 (bottom row, flipped)

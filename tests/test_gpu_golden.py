@@ -253,10 +253,13 @@ def test_cli_runs(tmp_path):
     import subprocess
     import sys
     r = subprocess.run([sys.executable, "-m", "montecarlopathtracing_amd", scenes.CFG, "--configid", "2",
-                        "--out", str(tmp_path), "--frames", "2"], cwd=scenes.ROOT, capture_output=True, text=True,
-                       timeout=300)
+                        "--out", str(tmp_path), "--frames", "2", "--preview", str(tmp_path / "cbox.png")],
+                       cwd=scenes.ROOT, capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stderr
     assert os.path.exists(tmp_path / "cbox.obj.hdr")
+    PIL = pytest.importorskip("PIL.Image")
+    with PIL.open(tmp_path / "cbox.png") as im:
+        assert im.size == (256, 256) and im.mode == "RGB"
 
 
 def _build_cases():
