@@ -147,7 +147,12 @@ constexpr int kQueues = 8;         // k_render work queues (at most): one per XC
 constexpr int kQueueStride = 32;   // u32 words between queue heads: one 128-B line each
 constexpr int kHandoffWords = 6;   // seed, mean.xyzw, count: one tagged 8-B granule each
 constexpr int kStatSlots = 24;
-constexpr int64_t kQuantAutoBytes = 32ll << 20;  // 8 XCDs x 4 MiB of L2     // k_render counters (mcpt_stats)
+constexpr int64_t kQuantAutoBytes = 32ll << 20;  // 8 XCDs x 4 MiB of L2
+// primary-hit pass: k_primary (one ray per lane) for search trees up to this
+// size, k_render's PRIM form (batched phases, resident grid) beyond: C3's
+// 0.24 MB tree 0.07 vs 0.13 ms, C2's 2.1 MB 0.18 vs 0.15, C5's 435 MB 3.57 vs
+// 1.66 (profiles/r02_primary_cache.txt)
+constexpr int64_t kPrimSmallTree = 1ll << 20;     // k_render counters (mcpt_stats)
 constexpr int kPhaseSlot = 16;     // MCPT_PHASE_TIMING: shader-clock ticks per phase (fetch, T, L, S)
 constexpr int kDebugSlot = 12;     // MCPT_DEBUG: violations of the stack bound, node and triangle indices
 
@@ -705,6 +710,7 @@ struct RenderArgs {
   int32_t *spill;             // WindowStack spill areas, one per resident lane
   int32_t spill_stride;       // entries per lane (stack depth - window)
   const PrimHit *prim;        // per-pixel primary hits (k_primary), nullptr: trace segment 0
+  PrimHit *prim_out;          // PRIM launches: where each pixel's primary hit goes
 };
 
 __device__ inline int32_t global_row(int32_t lr, const RenderArgs &A) {
@@ -740,7 +746,10 @@ __device__ inline uint32_t queue_items(uint32_t x, uint32_t n_tiles, uint32_t nq
 // run).  Expensive phases therefore execute with most of the wave active
 // instead of once per diverging lane.  Each lane's own
 // sequence of operations is exactly the reference's, so results are unchanged.
-template <int MODE, bool STATS, bool WIN, bool PAIR, bool Q>
+// PRIM: the primary-hit pass (PrimHit) run by the same machine: one frame,
+// no pixel state; a lane traces its pixel's primary ray, stores the closest
+// hit at the S phase instead of shading, and takes the next pixel.
+template <int MODE, bool STATS, bool WIN, bool PAIR, bool Q, bool PRIM = false>
 __global__ void __launch_bounds__(64, MCPT_WAVES_PER_SIMD) k_render(RenderArgs A) {
   constexpr bool PRUNE = MODE != MCPT_MODE_NOPRUNE;
   constexpr bool LIT = MODE == MCPT_MODE_NOPRUNE;
@@ -922,7 +931,8 @@ __global__ void __launch_bounds__(64, MCPT_WAVES_PER_SIMD) k_render(RenderArgs A
       if (lst == kPend) {  // start the entry once its pixel's previous block is published
         const int32_t pp = (int32_t)(pxy >> 16) * A.W + (int32_t)(pxy & 0xFFFFu);
         bool ready = true;
-        if (blk == 0) {  // state from before this launch
+        if (PRIM) {  // no pixel state: only the primary ray
+        } else if (blk == 0) {  // state from before this launch
           seed = A.seeds[pp];
           hist = A.hist[pp];
           cnt = A.count[pp];
@@ -1115,6 +1125,13 @@ __global__ void __launch_bounds__(64, MCPT_WAVES_PER_SIMD) k_render(RenderArgs A
         best_t = kFltMax;
         sp = 0;
         cur = S.root_leaf >= 0 ? ~S.root_leaf : 0;  // the root box passed: there were hits
+      } else if (PRIM && in_s) {
+        PrimHit h;
+        h.nrm = best_t < kFltMax ? best_nrm : (f4){0.0f, 0.0f, 0.0f, 0.0f};
+        h.t = best_t;
+        h.pad[0] = h.pad[1] = h.pad[2] = 0;
+        A.prim_out[(size_t)(pxy >> 16) * (size_t)A.W + (pxy & 0xFFFFu)] = h;
+        lst = kNeed;
       } else if (in_s) {
         if (STATS) n_seg++;
         bool done, fresh = false;
@@ -1961,6 +1978,12 @@ int mcpt_render_frames(mcpt_ctx *ctx, const mcpt_scene *scene, const mcpt_camera
                         {MCPT_KR(M, true, false, QN), MCPT_KR(M, true, true, QN)}}
   static const void *const kfns[3][2][2][2] = {MCPT_KK(MCPT_MODE_EXACT, false), MCPT_KK(MCPT_MODE_NOPRUNE, false),
                                                MCPT_KK(MCPT_MODE_EXACT, true)};
+  // the primary-hit pass: [kind][window][pair], no stats
+#define MCPT_KP(M, W, QN) {(const void *)k_render<M, false, W, false, QN, true>, (const void *)k_render<M, false, W, true, QN, true>}
+  static const void *const kpfns[3][2][2] = {{MCPT_KP(MCPT_MODE_EXACT, false, false), MCPT_KP(MCPT_MODE_EXACT, true, false)},
+                                             {MCPT_KP(MCPT_MODE_NOPRUNE, false, false), MCPT_KP(MCPT_MODE_NOPRUNE, true, false)},
+                                             {MCPT_KP(MCPT_MODE_EXACT, false, true), MCPT_KP(MCPT_MODE_EXACT, true, true)}};
+#undef MCPT_KP
 #undef MCPT_KK
 #undef MCPT_KR
   // quantized search tree: forced on (1) or off (2), or auto (0): on when the
@@ -2046,11 +2069,11 @@ int mcpt_render_frames(mcpt_ctx *ctx, const mcpt_scene *scene, const mcpt_camera
       1, std::min<int64_t>({(int64_t)INT32_MAX / std::max<uint32_t>(n_items, 1), 4096 / fpl + 1, 4095}));
   const int64_t n_blocks_all = (p->frames + fpl - 1) / fpl;
   const int n_launch = (int)((n_blocks_all + max_blocks - 1) / max_blocks);
-  if (n_launch > ctx->queue_cap) {  // kQueues heads per launch, zeroed by a single memset
+  if (n_launch + 1 > ctx->queue_cap) {  // kQueues heads per launch (+ the primary pass), zeroed by memsets
     if (ctx->d_queue) HIP_OK(hipFree(ctx->d_queue));
     ctx->d_queue = nullptr;
     ctx->queue_cap = 0;
-    const int cap = std::max(n_launch, 64);
+    const int cap = std::max(n_launch + 1, 64);
     HIP_OK(hipMalloc(&ctx->d_queue, (size_t)cap * kQueues * kQueueStride * sizeof(uint32_t)));
     ctx->queue_cap = cap;
   }
@@ -2076,6 +2099,7 @@ int mcpt_render_frames(mcpt_ctx *ctx, const mcpt_scene *scene, const mcpt_camera
   // previous call (the reference's one frame per update()); 1 always, 2
   // never.  Speed only: the same bits either way.
   A.prim = nullptr;
+  A.prim_out = nullptr;
   int prim_state = 0;
   if (T.primary_cache != 2 && tiles > 0 && p->frames > 0) {
     PrimKey key;
@@ -2103,13 +2127,46 @@ int mcpt_render_frames(mcpt_ctx *ctx, const mcpt_scene *scene, const mcpt_camera
           HIP_OK(hipMalloc(&ctx->d_prim, (size_t)n_px * sizeof(PrimHit)));
           ctx->prim_cap = n_px;
         }
-        const size_t lds_p = (size_t)depth_entries * 64 * sizeof(int32_t);
-        const dim3 g((unsigned)tiles);  // 8x8 pixel tiles of this rank's rows
-        if (noprune)
-          hipLaunchKernelGGL(k_primary<MCPT_MODE_NOPRUNE>, g, dim3(64), lds_p, st, A, ctx->d_prim);
-        else
-          hipLaunchKernelGGL(k_primary<MCPT_MODE_EXACT>, g, dim3(64), lds_p, st, A, ctx->d_prim);
-        HIP_OK(hipGetLastError());
+        if (scene->near4_bytes <= kPrimSmallTree) {
+          // small trees: one ray per lane, one 8x8 tile per workgroup
+          const size_t lds_p = (size_t)depth_entries * 64 * sizeof(int32_t);
+          const dim3 g((unsigned)tiles);
+          if (noprune)
+            hipLaunchKernelGGL(k_primary<MCPT_MODE_NOPRUNE>, g, dim3(64), lds_p, st, A, ctx->d_prim);
+          else
+            hipLaunchKernelGGL(k_primary<MCPT_MODE_EXACT>, g, dim3(64), lds_p, st, A, ctx->d_prim);
+          HIP_OK(hipGetLastError());
+        } else {
+        // the same persistent machine in its PRIM form: one frame, no state;
+        // its own queue heads (the slot after the render launches')
+        RenderArgs Ap = A;
+        Ap.frame_begin = 0;
+        Ap.frames = 1;
+        Ap.fpl = 1;
+        Ap.blocks = 1;
+        Ap.prim = nullptr;
+        Ap.prim_out = ctx->d_prim;
+        Ap.queue = ctx->d_queue + (size_t)n_launch * kQueues * kQueueStride;
+        HIP_OK(hipMemsetAsync(Ap.queue, 0, (size_t)kQueues * kQueueStride * sizeof(uint32_t), st));
+        // its own resident grid: the PRIM form needs fewer registers
+        const void *pfn = kpfns[kind][win][pair];
+        int per_cu_p = 0;
+        rc = occupancy(ctx, pfn, lds, &per_cu_p);
+        if (rc) return rc;
+        const int64_t grid_p = std::max<int64_t>(1, std::min<int64_t>(tiles, (int64_t)std::max(per_cu_p, 1) * ctx->n_cu));
+        const int64_t spill_p = win ? grid_p * 64 * (int64_t)A.spill_stride : 0;
+        if (spill_p > ctx->spill_cap) {
+          if (ctx->d_spill) HIP_OK(hipFree(ctx->d_spill));
+          ctx->d_spill = nullptr;
+          ctx->spill_cap = 0;
+          HIP_OK(hipMalloc(&ctx->d_spill, (size_t)spill_p * sizeof(int32_t)));
+          ctx->spill_cap = spill_p;
+          A.spill = ctx->d_spill;
+        }
+        Ap.spill = ctx->d_spill;
+        void *pargs[] = {&Ap};
+        HIP_OK(hipLaunchKernel(pfn, dim3((unsigned)grid_p), dim3(64), pargs, lds, st));
+        }
         HIP_OK(hipEventRecord(ctx->ev_prim, st));
         ctx->prim_key = key;
         ctx->prim_valid = true;
