@@ -1536,7 +1536,7 @@ int mcpt_get_stats(mcpt_ctx *c, mcpt_stats *out) {
     float ms = 0.0f;
     HIP_OK(hipEventElapsedTime(&ms, c->ev0, c->ev1));
     c->last.kernel_ms = ms;
-    if (c->last.primary_cache == 2) {  // k_primary's share of kernel_ms
+    if (c->last.primary_cache == 2) {  // the primary-hit pass's share of kernel_ms
       HIP_OK(hipEventElapsedTime(&ms, c->ev0, c->ev_prim));
       c->last.primary_ms = ms;
     }
@@ -2137,35 +2137,35 @@ int mcpt_render_frames(mcpt_ctx *ctx, const mcpt_scene *scene, const mcpt_camera
             hipLaunchKernelGGL(k_primary<MCPT_MODE_EXACT>, g, dim3(64), lds_p, st, A, ctx->d_prim);
           HIP_OK(hipGetLastError());
         } else {
-        // the same persistent machine in its PRIM form: one frame, no state;
-        // its own queue heads (the slot after the render launches')
-        RenderArgs Ap = A;
-        Ap.frame_begin = 0;
-        Ap.frames = 1;
-        Ap.fpl = 1;
-        Ap.blocks = 1;
-        Ap.prim = nullptr;
-        Ap.prim_out = ctx->d_prim;
-        Ap.queue = ctx->d_queue + (size_t)n_launch * kQueues * kQueueStride;
-        HIP_OK(hipMemsetAsync(Ap.queue, 0, (size_t)kQueues * kQueueStride * sizeof(uint32_t), st));
-        // its own resident grid: the PRIM form needs fewer registers
-        const void *pfn = kpfns[kind][win][pair];
-        int per_cu_p = 0;
-        rc = occupancy(ctx, pfn, lds, &per_cu_p);
-        if (rc) return rc;
-        const int64_t grid_p = std::max<int64_t>(1, std::min<int64_t>(tiles, (int64_t)std::max(per_cu_p, 1) * ctx->n_cu));
-        const int64_t spill_p = win ? grid_p * 64 * (int64_t)A.spill_stride : 0;
-        if (spill_p > ctx->spill_cap) {
-          if (ctx->d_spill) HIP_OK(hipFree(ctx->d_spill));
-          ctx->d_spill = nullptr;
-          ctx->spill_cap = 0;
-          HIP_OK(hipMalloc(&ctx->d_spill, (size_t)spill_p * sizeof(int32_t)));
-          ctx->spill_cap = spill_p;
-          A.spill = ctx->d_spill;
-        }
-        Ap.spill = ctx->d_spill;
-        void *pargs[] = {&Ap};
-        HIP_OK(hipLaunchKernel(pfn, dim3((unsigned)grid_p), dim3(64), pargs, lds, st));
+          // the same persistent machine in its PRIM form: one frame, no state;
+          // its own queue heads (the slot after the render launches')
+          RenderArgs Ap = A;
+          Ap.frame_begin = 0;
+          Ap.frames = 1;
+          Ap.fpl = 1;
+          Ap.blocks = 1;
+          Ap.prim = nullptr;
+          Ap.prim_out = ctx->d_prim;
+          Ap.queue = ctx->d_queue + (size_t)n_launch * kQueues * kQueueStride;
+          HIP_OK(hipMemsetAsync(Ap.queue, 0, (size_t)kQueues * kQueueStride * sizeof(uint32_t), st));
+          // its own resident grid: the PRIM form needs fewer registers
+          const void *pfn = kpfns[kind][win][pair];
+          int per_cu_p = 0;
+          rc = occupancy(ctx, pfn, lds, &per_cu_p);
+          if (rc) return rc;
+          const int64_t grid_p = std::max<int64_t>(1, std::min<int64_t>(tiles, (int64_t)std::max(per_cu_p, 1) * ctx->n_cu));
+          const int64_t spill_p = win ? grid_p * 64 * (int64_t)A.spill_stride : 0;
+          if (spill_p > ctx->spill_cap) {
+            if (ctx->d_spill) HIP_OK(hipFree(ctx->d_spill));
+            ctx->d_spill = nullptr;
+            ctx->spill_cap = 0;
+            HIP_OK(hipMalloc(&ctx->d_spill, (size_t)spill_p * sizeof(int32_t)));
+            ctx->spill_cap = spill_p;
+            A.spill = ctx->d_spill;
+          }
+          Ap.spill = ctx->d_spill;
+          void *pargs[] = {&Ap};
+          HIP_OK(hipLaunchKernel(pfn, dim3((unsigned)grid_p), dim3(64), pargs, lds, st));
         }
         HIP_OK(hipEventRecord(ctx->ev_prim, st));
         ctx->prim_key = key;
