@@ -222,6 +222,8 @@ def main():
                          "when --schedule is auto, else the default")
     ap.add_argument("--fetch-threshold", type=int, default=0,
                     help="k_render fetch threshold (mcpt_tuning.fetch_threshold); 0: tuned like the S threshold")
+    ap.add_argument("--block-entries", type=int, default=0,
+                    help="k_render block sizing (mcpt_tuning.block_entries); 0: tuned like the S threshold")
     args = ap.parse_args()
     global W, H_PER_GPU, DEPTH
     wl = WORKLOADS[args.workload]
@@ -260,6 +262,8 @@ def main():
         rnd.set_tuning(**dict(rnd.get_tuning(), shade_threshold=args.shade_threshold))
     if args.fetch_threshold > 0:
         rnd.set_tuning(**dict(rnd.get_tuning(), fetch_threshold=args.fetch_threshold))
+    if args.block_entries > 0:
+        rnd.set_tuning(**dict(rnd.get_tuning(), block_entries=args.block_entries))
     shade_th = rnd.get_tuning()["shade_threshold"] or 32
     if args.schedule == "auto" and args.shade_threshold > 0:
         rnd.tune_schedule(dsc, cam, st, DEPTH, attempt, frames=max(1, min(args.steps, 64)), trials=3, **kw)
@@ -371,6 +375,7 @@ def main():
                           "schedule": "paired" if dsc.schedule == L.SCHED_PAIRED else "single",
                           "shade_threshold": shade_th,
                           "fetch_threshold": rnd.get_tuning()["fetch_threshold"] or 1,
+                          "block_entries": rnd.get_tuning()["block_entries"] or 32,
                           "frames_per_block": fpb, "search_tree_nodes": search_tree},
                "active_Msegments_per_s": round(segments * n / elapsed / 1e6, 2),
                "image_reduce_ms": None if reduce_ms is None else round(reduce_ms, 3),

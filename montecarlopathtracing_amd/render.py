@@ -201,14 +201,15 @@ class Renderer:
         return sched, {k[0]: v for k, v in best.items()}
 
     def tune(self, scene, camera, state, max_depth, max_attempt, frames=64, trials=1, shade_thresholds=(32, 40, 48),
-             fetch_thresholds=(1, 8), **kw):
+             fetch_thresholds=(1, 8), block_entries=(12, 32), **kw):
         """tune_schedule over the leaf-test schedule, the S-phase threshold
         (mcpt_tuning.shade_threshold) and then the fetch threshold
-        (mcpt_tuning.fetch_threshold): their best values differ by scene
-        (veach_mis: S 48, fetch 8; cbox: 40, 8; the 10 M-triangle soup: 32, 1).
-        Every combination gives the same bits.  The winner goes to
-        scene.schedule and the renderer's tuning.  Returns (schedule,
-        shade_threshold, {(schedule, shade, fetch): best ms})."""
+        (mcpt_tuning.fetch_threshold), then the block sizing
+        (mcpt_tuning.block_entries): their best values differ by scene
+        (veach_mis: S 48, fetch 8, 12 entries; cbox: 32-40, 8; the 10 M-triangle
+        soup: 32, 1, 32 entries).  Every combination gives the same bits.  The
+        winner goes to scene.schedule and the renderer's tuning.  Returns
+        (schedule, shade_threshold, {(schedule, shade, fetch, entries): best ms})."""
         if getattr(self, "_stats_on", False):
             raise L.MCPTError("tune: counters must be off (they change the kernel)")
         base = self.get_tuning()
@@ -217,32 +218,39 @@ class Renderer:
         scratch.width, scratch.height, scratch.frames_done = state.width, state.height, state.frames_done
         best = {}
 
-        def trial(sched, th, fe):
-            self.set_tuning(**dict(base, shade_threshold=th, fetch_threshold=fe))
+        def trial(sched, th, fe, be):
+            self.set_tuning(**dict(base, shade_threshold=th, fetch_threshold=fe, block_entries=be))
             scratch.seeds, scratch.hist, scratch.count = state.seeds.clone(), state.hist.clone(), state.count.clone()
             self.render_frames(scene, camera, scratch, max_depth, max_attempt, frames,
                                frame_begin=state.frames_done, schedule=sched, **kw)
             ms = self.stats()["kernel_ms"]
-            best[(sched, th, fe)] = min(best.get((sched, th, fe), ms), ms)
+            best[(sched, th, fe, be)] = min(best.get((sched, th, fe, be), ms), ms)
 
         fe0 = base["fetch_threshold"] or 1  # 0 = the default, 1
+        be0 = base["block_entries"] or 32   # 0 = the default, 32
         try:
             for _ in range(int(trials)):
                 for th in ths:
                     for sched in (L.SCHED_SINGLE, L.SCHED_PAIRED):
-                        trial(sched, th, fe0)
-            sched, th, fe = min(best, key=lambda k: (best[k], k))
+                        trial(sched, th, fe0, be0)
+            sched, th, fe, be = min(best, key=lambda k: (best[k], k))
             if shade_thresholds and fetch_thresholds:  # then the fetch threshold, with that pair
                 for _ in range(int(trials)):
                     for f in fetch_thresholds:
                         if f != fe0:
-                            trial(sched, th, f)
-                sched, th, fe = min(best, key=lambda k: (best[k], k))
+                            trial(sched, th, f, be0)
+                sched, th, fe, be = min(best, key=lambda k: (best[k], k))
+            if shade_thresholds and block_entries:  # then the block sizing
+                for _ in range(int(trials)):
+                    for b in block_entries:
+                        if b != be0:
+                            trial(sched, th, fe, b)
+                sched, th, fe, be = min(best, key=lambda k: (best[k], k))
         finally:
             self.set_tuning(**base)
         scene.schedule = sched
         if shade_thresholds:
-            self.set_tuning(**dict(base, shade_threshold=th, fetch_threshold=fe))
+            self.set_tuning(**dict(base, shade_threshold=th, fetch_threshold=fe, block_entries=be))
         return sched, th, best
 
     # ------------------------------------------------ wavefront (drop-in)

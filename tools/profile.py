@@ -75,7 +75,8 @@ def run(tag, args):
     # every pass profiles the same kernel instantiation
     cfg = json.loads(line.splitlines()[-1])["config"]
     quiet = bench + ["--no-cpu", "--schedule", cfg["schedule"], "--shade-threshold", str(cfg.get("shade_threshold", 32)),
-                     "--fetch-threshold", str(cfg.get("fetch_threshold", 1))]
+                     "--fetch-threshold", str(cfg.get("fetch_threshold", 1)),
+                     "--block-entries", str(cfg.get("block_entries", 32))]
     sh(["rocprofv3", "--kernel-trace", "--stats", "--output-format", "csv", "-d", os.path.join(out, "trace"), "--"]
        + quiet, os.path.join(out, "trace.log"), 400)
     print("trace done", flush=True)
