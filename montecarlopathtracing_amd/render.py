@@ -201,13 +201,13 @@ class Renderer:
         return sched, {k[0]: v for k, v in best.items()}
 
     def tune(self, scene, camera, state, max_depth, max_attempt, frames=64, trials=1, shade_thresholds=(32, 40, 48),
-             fetch_thresholds=(1, 8), block_entries=(12, 32), **kw):
+             fetch_thresholds=(1, 8), block_entries=(8, 32), **kw):
         """tune_schedule over the leaf-test schedule, the S-phase threshold
         (mcpt_tuning.shade_threshold) and then the fetch threshold
         (mcpt_tuning.fetch_threshold), then the block sizing
         (mcpt_tuning.block_entries): their best values differ by scene
-        (veach_mis: S 48, fetch 8, 12 entries; cbox: 32-40, 8; the 10 M-triangle
-        soup: 32, 1, 32 entries).  Every combination gives the same bits.  The
+        (veach_mis: S 40, fetch 8, 8 entries; cbox: 32-40, 8, 32; the 10 M-triangle
+        soup: 32, 1, 32).  Every combination gives the same bits.  The
         winner goes to scene.schedule and the renderer's tuning.  Returns
         (schedule, shade_threshold, {(schedule, shade, fetch, entries): best ms})."""
         if getattr(self, "_stats_on", False):
@@ -246,6 +246,12 @@ class Renderer:
                         if b != be0:
                             trial(sched, th, fe, b)
                 sched, th, fe, be = min(best, key=lambda k: (best[k], k))
+                if be != be0:  # other blocks move the best S threshold (C3: 48 -> 40)
+                    for _ in range(int(trials)):
+                        for t in ths:
+                            if t != th:
+                                trial(sched, t, fe, be)
+                    sched, th, fe, be = min(best, key=lambda k: (best[k], k))
         finally:
             self.set_tuning(**base)
         scene.schedule = sched
