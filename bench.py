@@ -342,7 +342,12 @@ def main():
             roof["traffic"] = traffic
             roof["achieved"] = round(traffic / avg_launch_s / 1e9, 2)
             roof["frac"] = round(roof["achieved"] / HBM_PEAK_GBS, 5)
-            roof["issue_frac"] = prof.get("valu_busy")
+            # rocprofv3's VALUBusy definition reads up to ~1 % over 1 on a saturated
+            # kernel (C3); the fraction is capped, the raw counter ratio kept beside it
+            vb = prof.get("valu_busy")
+            roof["issue_frac"] = None if vb is None else min(1.0, vb)
+            if vb is not None and vb > 1.0:
+                roof["issue_frac_raw"] = vb
             roof["td_busy"] = prof.get("td_busy")
             roof["binding"] = ("vector-memory gathers: TD (data-return) busy %s of the kernel's cycles, VALU issue %s "
                                "(DESIGN.md §3.6; profiles/r02_probe_ab.txt)" % (prof.get("td_busy"), prof.get("valu_busy")))
