@@ -358,6 +358,23 @@ int mcpt_build_hlbvh_device(const mcpt_triangle *tris_dev, int64_t n, mcpt_bvh_n
  * Synchronises `stream`.                                                  */
 int mcpt_treelet_device(mcpt_bvh_node *nodes_dev, int64_t n_nodes, void *stream);
 
+/* TreeletBVH<GPU> (MCPT/BVH/treeletBVH.cpp:413-438 + kernels/treeletBVH.cl:230-531):
+ * the GPU treelet kernel the reference runs on a fresh HLBVH for EVERY
+ * bvhtype before rendering (SceneCL's ctor falls through into its GPUBVH
+ * block, scenebuild.cpp:66-95), so the tree its intersect kernel reads.  In
+ * place on a DEVICE array of 2n-1 nodes in the HLBVH layout (internal nodes
+ * [0, n-2], leaves [n-1, 2n-2]).  The kernel's warp-synchronous behaviour is
+ * restated deterministically: its pickNode argmax, lockstep
+ * reductions and tie stores (highest lane lands), its refit SAH without
+ * /rootArea (treeletBVH.cl:524-525), FP as ROCm's OpenCL compiler builds it
+ * for gfx950.  Parity unpinned (treeletBVH.cl:80-81 does not compile).
+ * Synchronises `stream`.                                                  */
+int mcpt_treelet_gpu_device(mcpt_bvh_node *nodes_dev, int64_t n_nodes, void *stream);
+/* Same on a HOST array, the way the reference host uses it on its own node
+ * vector (upload, restructure, read back; scenebuild.cpp:89-94,
+ * bvhtest.cpp:503-511), on the calling thread's current device.           */
+int mcpt_treelet_gpu(mcpt_bvh_node *nodes, int64_t n_nodes);
+
 /* BVH quality metrics of "testbvh" (bvhtest.cpp:448-530), on the GPU.
  * EPO_GPU (bvhtest.cpp:288-321 + kernels/EPO.cl:133-197): per-triangle EPO
  * area and triangle area into the caller's DEVICE arrays (n_tris floats

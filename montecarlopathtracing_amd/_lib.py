@@ -109,6 +109,8 @@ SIGNATURES = {
     "mcpt_gather_probe": (_I32, [_P, _I32, _I64, _P]),
     "mcpt_build_hlbvh_device": (_I32, [_P, _I64, _P, _P]),
     "mcpt_treelet_device": (_I32, [_P, _I64, _P]),
+    "mcpt_treelet_gpu_device": (_I32, [_P, _I64, _P]),
+    "mcpt_treelet_gpu": (_I32, [_P, _I64]),
     "mcpt_bvh_sah": (_I32, [_P, _I64, _P]),
     "mcpt_bvh_epo_device": (_I32, [_P, _P, _I64, _P, _P, _P, _P, _P]),
     "mcpt_bvh_lcv_device": (_I32, [_P, _I64, _P, _I32, _I32, _P, _P, _P]),

@@ -49,15 +49,16 @@ class App:
         if not directory.endswith("/"):
             directory += "/"
         self.data = S.SceneData.from_obj(directory, self.cfg.GETOBJNAME(), self.material_override)
-        # SceneCL ctor (scenebuild.cpp:66-79): HLBVH, optionally restructured
-        # by the treelet pass.  "treeletGPU" runs the reference's GPU kernel
-        # (treeletBVH.cl), whose result depends on warp-synchronous races; both
-        # names run TreeletBVH<CPU>'s deterministic pass here.
+        # SceneCL ctor (scenebuild.cpp:66-95): whatever bvhtype names, the
+        # "hlbvh" and "treelet" branches fall through into the GPUBVH block
+        # ("treeletGPU" jumps there), which uploads a FRESH HLBVH over bvhBuffer
+        # and restructures it in place with the GPU treelet kernel; intersect
+        # reads that buffer (:125).  "treelet"'s TreeletBVH<CPU> tree (:70-73)
+        # is built and then overwritten, so it is not computed here.
         bvhtype = self.cfg.BVHTYPE()
-        if bvhtype in ("treelet", "treeletGPU"):
-            self.data = self.data.with_nodes(R.treelet_device(self.data.nodes, self.device))
-        elif bvhtype != "hlbvh":
-            raise ValueError("BVH Not Implemented: %r" % bvhtype)  # scenebuild.cpp:78
+        if bvhtype not in ("hlbvh", "treelet", "treeletGPU"):
+            raise ValueError("BVH Not Implemented: %r" % bvhtype)  # scenebuild.cpp:77-79
+        self.data = self.data.with_nodes(R.treelet_gpu_device(self.data.nodes, self.device))
         self.camera = S.parse_camera(cam)
         self.renderer = R.Renderer(self.device)
         self.scene = self.renderer.upload(self.data)

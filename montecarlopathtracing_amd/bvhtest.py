@@ -6,8 +6,10 @@ print its quality metrics.
     EPO_GPU  bvhtest.cpp:288-321  GPU, kernels/EPO.cl restated (mcpt_bvh_epo_device)
     LCV      bvhtest.cpp:324-444  GPU (mcpt_bvh_lcv_device), when the config has a camera
 
-The BVH is the reference's: HLBVH<CPU> (host build, hlbvh.cpp) for "hlbvh",
-then TreeletBVH<CPU> on the GPU for "treelet" / "treeletGPU" (DESIGN.md §3.8).
+The BVH is the reference's (bvhtest.cpp:458-519): HLBVH<CPU> (host build,
+hlbvh.cpp) for "hlbvh"; TreeletBVH<CPU>'s pass over it for "treelet" (run on
+the GPU); the GPU treelet kernel's pass, TreeletBVH<GPU>
+(treeletBVH.cl), for "treeletGPU".
 Output lines follow the reference's std::cout lines.
 """
 import ctypes
@@ -29,9 +31,12 @@ def load_triangles(directory, objname):
 
 def build(tris, bvhtype="hlbvh", device=0):
     nodes = S.build_hlbvh(tris)
-    if bvhtype in ("treelet", "treeletGPU"):
+    if bvhtype == "treelet":
         from . import render as R
         nodes = R.treelet_device(nodes, device)
+    elif bvhtype == "treeletGPU":
+        from . import render as R
+        nodes = R.treelet_gpu_device(nodes, device)
     elif bvhtype != "hlbvh":
         raise ValueError("BVH Not Implemented: %r" % bvhtype)
     return nodes

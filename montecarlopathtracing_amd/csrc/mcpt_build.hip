@@ -536,6 +536,45 @@ __global__ __launch_bounds__(64) void k_tl_rebuild(const int32_t *__restrict__ l
     }                                                                                        \
   } while (0)
 
+namespace mcpt {
+// Depth groups of the internal nodes of a 2n-1-node tree rooted at 0, top-down:
+// lv[off[k] .. off[k+1]) holds depth k.  lv needs n-1 entries, cnt one word.
+// Shared by both treelet passes (this file, mcpt_treelet_gpu.hip).
+int tree_levels(const mcpt_bvh_node *nodes, int64_t n, hipStream_t st, int32_t *lv, uint32_t *cnt,
+                std::vector<uint32_t> &off) {
+  int rc = MCPT_OK;
+  const int32_t zero = 0;
+  off.clear();
+  TL_OK(hipMemcpyAsync(lv, &zero, sizeof(int32_t), hipMemcpyHostToDevice, st));
+  off.push_back(0);
+  off.push_back(1);
+  for (;;) {
+    const uint32_t a = off[off.size() - 2], b = off.back();
+    if (b == a) break;
+    if (b > (uint32_t)(n - 1)) {
+      rc = mcpt::fail(MCPT_ERR_ARG, "treelet_device: node links do not form a tree");
+      goto done;
+    }
+    TL_OK(hipMemsetAsync(cnt, 0, sizeof(uint32_t), st));
+    hipLaunchKernelGGL(k_tl_expand, dim3(blocks_for(b - a, 256)), dim3(256), 0, st, lv + a, b - a, nodes, lv + b, cnt);
+    TL_OK(hipGetLastError());
+    uint32_t c = 0;
+    TL_OK(hipMemcpyAsync(&c, cnt, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+    TL_OK(hipStreamSynchronize(st));
+    if ((uint64_t)b + c > (uint64_t)(n - 1)) {
+      rc = mcpt::fail(MCPT_ERR_ARG, "treelet_device: node links do not form a tree");
+      goto done;
+    }
+    off.push_back(b + c);
+  }
+  off.pop_back();  // the empty group
+  if (off.back() != (uint32_t)(n - 1))
+    rc = mcpt::fail(MCPT_ERR_ARG, "treelet_device: expected n-1 internal nodes reachable from the root");
+done:
+  return rc;
+}
+}  // namespace mcpt
+
 extern "C" int mcpt_treelet_device(mcpt_bvh_node *nodes, int64_t n_nodes, void *stream) {
   if (!nodes || n_nodes <= 0 || (n_nodes & 1) == 0)
     return mcpt::fail(MCPT_ERR_ARG, "treelet_device: expected a 2n-1-node BVH");
@@ -566,37 +605,8 @@ extern "C" int mcpt_treelet_device(mcpt_bvh_node *nodes, int64_t n_nodes, void *
     goto done;
   }
   root_area = tl_area_host(root_h);  // ::rootArea, fixed before any rebuild (:351)
-  {
-    // depth groups of internal nodes, top-down
-    const int32_t zero = 0;
-    TL_OK(hipMemcpyAsync(lv, &zero, sizeof(int32_t), hipMemcpyHostToDevice, st));
-    off.push_back(0);
-    off.push_back(1);
-    for (;;) {
-      const uint32_t a = off[off.size() - 2], b = off.back();
-      if (b == a) break;
-      if (b > (uint32_t)(n - 1)) {
-        rc = mcpt::fail(MCPT_ERR_ARG, "treelet_device: node links do not form a tree");
-        goto done;
-      }
-      TL_OK(hipMemsetAsync(cnt, 0, sizeof(uint32_t), st));
-      hipLaunchKernelGGL(k_tl_expand, dim3(blocks_for(b - a, 256)), dim3(256), 0, st, lv + a, b - a, nodes, lv + b,
-                         cnt);
-      TL_OK(hipGetLastError());
-      uint32_t c = 0;
-      TL_OK(hipMemcpyAsync(&c, cnt, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
-      TL_OK(hipStreamSynchronize(st));
-      if ((uint64_t)b + c > (uint64_t)(n - 1)) {
-        rc = mcpt::fail(MCPT_ERR_ARG, "treelet_device: node links do not form a tree");
-        goto done;
-      }
-      off.push_back(b + c);
-    }
-    if (off.back() != (uint32_t)(n - 1)) {
-      rc = mcpt::fail(MCPT_ERR_ARG, "treelet_device: expected n-1 internal nodes reachable from the root");
-      goto done;
-    }
-  }
+  rc = mcpt::tree_levels(nodes, n, st, lv, cnt, off);  // depth groups of internal nodes, top-down
+  if (rc != MCPT_OK) goto done;
   // getInformation (:343-347)
   hipLaunchKernelGGL(k_tl_mark_path, dim3(1), dim3(64), 0, st, nodes, n, on_path, err);
   TL_OK(hipGetLastError());

@@ -342,3 +342,16 @@ def treelet_device(nodes, device=0):
     n = d.numel() // L.BVHNODE.itemsize
     L.check(L.lib().mcpt_treelet_device(L.ptr(d), n, _stream()))
     return records(d, L.BVHNODE).copy() if host else d
+
+
+def treelet_gpu_device(nodes, device=0):
+    """TreeletBVH<GPU> (MCPT/BVH/treeletBVH.cpp:413-438, kernels/treeletBVH.cl),
+    the tree every reference render traverses (scenebuild.cpp:87-95), run by
+    mcpt_treelet_gpu_device.  `nodes` is a host BVHNODE array in the HLBVH
+    layout (returns a restructured host copy) or a device byte tensor
+    (restructured in place and returned)."""
+    host = isinstance(nodes, np.ndarray)
+    d = to_device(nodes, device) if host else nodes
+    n = d.numel() // L.BVHNODE.itemsize
+    L.check(L.lib().mcpt_treelet_gpu_device(L.ptr(d), n, _stream()))
+    return records(d, L.BVHNODE).copy() if host else d

@@ -51,6 +51,17 @@ void oracle_set_prune(int on);
  * HLBVH; mcpt_oracle_treelet.cpp.  0 ok, -1 the reference's recursion would
  * not terminate on this tree, -2 bad argument. */
 int oracle_treelet(mcpt_bvh_node *nodes, int64_t n_nodes);
+/* TreeletBVH<GPU> (treeletBVH.cpp:413-438 + kernels/treeletBVH.cl:230-531), the
+ * tree every reference render traverses (scenebuild.cpp:87-95), in place on a
+ * 2n-1-node HLBVH; mcpt_oracle_treelet_gpu.cpp (PARITY UNPINNED: the kernel
+ * does not compile).  rcp_mant_root_bits: v_rcp_f32(frexp_mant(rootArea)) as
+ * float bits (0: the correctly rounded reciprocal); options 0 = the kernel
+ * (bit 0: the lowest lane's store lands instead of the highest's; bit 1:
+ * refit SAH divided by rootArea — sensitivity knobs, not the reference);
+ * stats[8] optional.  0 ok, -1 not an HLBVH layout, -2 bad argument. */
+int oracle_treelet_gpu(mcpt_bvh_node *nodes, int64_t n_nodes, uint32_t rcp_mant_root_bits, int32_t options,
+                       int64_t *stats);
+float oracle_treelet_gpu_root_mant(const mcpt_bvh_node *root);
 /* testbvh metrics (bvhtest.cpp): SAH :97-108, LCV :324-444 (counts optional,
  * index i*H + j), EPO_GPU's kernel EPO.cl:133-197 per triangle. */
 float oracle_bvh_sah(const mcpt_bvh_node *nodes, int64_t n_nodes);

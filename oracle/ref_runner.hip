@@ -99,6 +99,11 @@ struct Dev {
     if ((x) != 0) return -1; \
   } while (0)
 
+__global__ void k_rcp_probe(float *x, int64_t n) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) x[i] = __builtin_amdgcn_rcpf(x[i]);
+}
+
 }  // namespace
 
 extern "C" {
@@ -291,6 +296,22 @@ int ref_epo(const mcpt_bvh_node *nodes, int64_t nn, const mcpt_triangle *tris, i
   CK(hipDeviceSynchronize());
   TRY(de.down(epo_out));
   TRY(da.down(area_out));
+  return 0;
+}
+
+// Hardware reciprocals (v_rcp_f32) of n floats.  treeletBVH.cl does not
+// compile, so its restatement (oracle/mcpt_oracle_treelet_gpu.cpp)
+// models the kernel's 2.5-ulp x / rootArea as frexp / v_rcp_f32 / ldexp, the
+// sequence ROCm's OpenCL compiler emits for gfx950, and takes v_rcp_f32's
+// value of frexp_mant(rootArea) from this probe.
+int ref_rcp_f32(const float *in, float *out, int64_t n) {
+  Dev<float> d;
+  TRY(d.alloc(n));
+  TRY(d.up(in));
+  hipLaunchKernelGGL(k_rcp_probe, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, 0, d.p, n);
+  CK(hipGetLastError());
+  CK(hipDeviceSynchronize());
+  TRY(d.down(out));
   return 0;
 }
 

@@ -165,7 +165,8 @@ struct App {
     max_attempt = (int32_t)c["attempt"].num;
     objname = c["objname"].str;
     const std::string bvhtype = c.has("bvhtype") ? c["bvhtype"].str : "hlbvh";
-    if (bvhtype != "hlbvh") throw std::runtime_error("this host builds the \"hlbvh\" tree only");
+    if (bvhtype != "hlbvh" && bvhtype != "treelet" && bvhtype != "treeletGPU")
+      throw std::runtime_error("BVH Not Implemented");  // scenebuild.cpp:77-79
     const Json &jc = c["camera"];
     if (jc.has("resolution") && ((int32_t)jc["resolution"][0].num != width || (int32_t)jc["resolution"][1].num != height))
       throw std::runtime_error("camera.resolution must equal width/height");
@@ -182,10 +183,13 @@ struct App {
     if (c.has("materials") && c["materials"].str == "diffuse_only")  // BASELINE C2's override
       for (auto &m : mats)
         if (m.type != MCPT_LIGHT) m.type = MCPT_DIFFUSE;
-    // SceneCL ctor: pack normals + material ids, HLBVH<CPU>, upload
+    // SceneCL ctor: pack normals + material ids, then (every bvhtype falls
+    // through into the GPUBVH block, scenebuild.cpp:87-95) a fresh HLBVH<CPU>
+    // restructured by TreeletBVH<GPU>, upload
     OK(mcpt_pack_triangles(tris.data(), mat_id.data(), n));
     std::vector<mcpt_bvh_node> nodes(2 * n - 1);
     OK(mcpt_build_hlbvh(tris.data(), n, nodes.data()));
+    OK(mcpt_treelet_gpu(nodes.data(), (int64_t)nodes.size()));
     OK(mcpt_scene_upload(ctx, tris.data(), n, nodes.data(), (int64_t)nodes.size(), mats.data(), nm, &scene));
     // Auxiliary::parseCamera
     double p[3], l[3], u[3];

@@ -109,6 +109,24 @@ def treelet(nodes):
     return rc, out
 
 
+def treelet_gpu(nodes, rcp_bits=0, options=0):
+    """TreeletBVH<GPU> (treeletBVH.cl) restated (oracle/mcpt_oracle_treelet_gpu.cpp):
+    (status, nodes, stats[8]).  rcp_bits: the GPU's v_rcp_f32(frexp_mant(rootArea))
+    as uint32 bits (0 = correctly rounded); options: bit 0 lowest-lane stores,
+    bit 1 refit divided by rootArea (sensitivity knobs, not the kernel)."""
+    out = np.ascontiguousarray(nodes).copy()
+    stats = np.zeros(8, np.int64)
+    rc = so().oracle_treelet_gpu(P(out), i64(len(out)), ctypes.c_uint32(int(rcp_bits)), i32(options), P(stats))
+    return rc, out, stats
+
+
+def root_area_mant(nodes):
+    """frexp mantissa of treeletBVH.cl's rootArea (AREA(nodes[0]), :245): the
+    float whose v_rcp_f32 the GPU tests feed to treelet_gpu()."""
+    so().oracle_treelet_gpu_root_mant.restype = ctypes.c_float
+    return np.float32(so().oracle_treelet_gpu_root_mant(P(np.ascontiguousarray(nodes[:1]))))
+
+
 def bvh_sah(nodes):
     return so().oracle_bvh_sah(P(np.ascontiguousarray(nodes)), i64(len(nodes)))
 

@@ -25,7 +25,8 @@ def so():
     if _so is None:
         s = ctypes.CDLL(os.path.join(REF_DIR, "libref_runner.so"))
         s.ref_last_error.restype = ctypes.c_char_p
-        for n in ("ref_init", "ref_generate", "ref_intersect", "ref_shade", "ref_accumulate", "ref_render", "ref_epo"):
+        for n in ("ref_init", "ref_generate", "ref_intersect", "ref_shade", "ref_accumulate", "ref_render", "ref_epo",
+                  "ref_rcp_f32"):
             getattr(s, n).restype = ctypes.c_int
         if s.ref_init(REF_DIR.encode()) != 0:
             raise RuntimeError(s.ref_last_error().decode())
@@ -89,3 +90,12 @@ def epo(nodes, tris):
     _ck(so().ref_epo(P(np.ascontiguousarray(nodes)), i64(len(nodes)), P(np.ascontiguousarray(tris)), i64(n), P(e),
                      P(a)))
     return e, a
+
+
+def rcp_f32(x):
+    """The GPU's v_rcp_f32 of each float (the hardware reciprocal the
+    treeletBVH.cl restatement's 2.5-ulp division uses)."""
+    a = np.ascontiguousarray(np.atleast_1d(x), np.float32).copy()
+    out = np.zeros_like(a)
+    _ck(so().ref_rcp_f32(P(a), P(out), i64(len(a))))
+    return out

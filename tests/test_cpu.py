@@ -379,6 +379,73 @@ def test_oracle_treelet_reports_the_reference_recursion_cycle():
     assert rc == -1
 
 
+def _random_tree(n, seed):
+    rng = np.random.default_rng(seed)
+    v = rng.uniform(0, 10, (n, 3, 3)).astype(np.float32)
+    t = np.zeros(len(v), L.TRIANGLE)
+    t["v"][:, :, :3] = v
+    tris = S.pack_triangles(t, np.zeros(len(v), np.int32))
+    return tris, S.build_hlbvh(tris)
+
+
+@pytest.mark.parametrize("name", ["cbox", "mis", "dining", "random"])
+def test_oracle_treelet_gpu_is_a_valid_tree_unlike_the_cpu_pass(name):
+    """TreeletBVH<GPU> restated (oracle/mcpt_oracle_treelet_gpu.cpp, the tree
+    every reference render traverses, scenebuild.cpp:87-95): a permutation of
+    the HLBVH's internal nodes over the same leaves, a lower SAH metric, and a
+    DIFFERENT tree from TreeletBVH<CPU>'s (array queue with pickNode's argmax,
+    reduction-based 6/7-leaf splits, refit without /rootArea)."""
+    if name == "random":
+        tris, nodes = _random_tree(3000, 3)
+    else:
+        data = getattr(scenes, name)()
+        tris, nodes = data.tris, data.nodes
+    rc, out, st = O.treelet_gpu(nodes)
+    assert rc == 0
+    n = len(tris)
+    assert (out["left"][n - 1:] == nodes["left"][n - 1:]).all()
+    assert (out["bbmin"][n - 1:] == nodes["bbmin"][n - 1:]).all()
+    _check_tree(out, n)
+    assert _sah_metric(out) < _sah_metric(nodes)
+    assert S.bvh_stack_depth(out) <= 64
+    assert st[0] > 0 and st[0] + st[5] == n - 1  # every internal node processed once
+    assert st[6] == 0  # no +-0 min/max ties: the v_min/v_max sign rule decides nothing here
+    if name != "dining":  # the proxy's leaf n-1 names an ancestor (TreeletBVH<CPU> refuses it)
+        rc2, cpu = O.treelet(nodes)
+        assert rc2 == 0 and cpu.tobytes() != out.tobytes()
+
+
+def test_treelet_gpu_missing_root_area_and_lane_rule_decide_the_tree():
+    """treeletBVH.cl:524-525 refits without /rootArea: rebuilt nodes carry
+    un-normalised costs that later pickNode / DP choices compare with
+    normalised ones.  Dividing there (TreeletBVH<CPU>'s :292-293 form) gives a
+    different cbox tree; so does letting the LOWEST lane's store land on
+    pickNode's maxNodeID / the 6-7-leaf popt (the restatement takes the
+    highest).  The quirk counters show each path runs."""
+    nodes = scenes.cbox().nodes
+    _, base, st = O.treelet_gpu(nodes)
+    _, norm, _ = O.treelet_gpu(nodes, options=2)
+    _, low, st_low = O.treelet_gpu(nodes, options=1)
+    assert base.tobytes() != norm.tobytes()
+    assert base.tobytes() != low.tobytes()
+    assert st[1] > 0 and st[2] > 0  # several lanes store maxNodeID; none does (stale value kept)
+    assert st_low[0] > st[0]  # the lowest-lane rule grows fuller treelets
+    # rcp parameter: the correctly rounded reciprocal is the default (bits 0)
+    m = O.root_area_mant(nodes)
+    r = np.float32(1.0) / m
+    _, same, _ = O.treelet_gpu(nodes, rcp_bits=int(r.view(np.uint32)))
+    assert same.tobytes() == base.tobytes()
+
+
+def test_treelet_gpu_argument_checks():
+    _, nodes = _random_tree(50, 1)
+    swapped = nodes.copy()
+    swapped[0]["left"], swapped[0]["right"] = nodes[0]["right"], nodes[0]["left"]
+    assert O.treelet_gpu(swapped)[0] == 0  # child order is free
+    assert O.treelet_gpu(nodes[:-1])[0] == -2  # even node count
+    assert O.treelet_gpu(nodes, options=4)[0] == -2
+
+
 # ------------------------------------------------------ testbvh metrics
 @pytest.mark.parametrize("name", ["cbox", "mis"])
 def test_sah_metric_product_equals_oracle(name):

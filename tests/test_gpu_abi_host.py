@@ -54,7 +54,10 @@ def _state(tmp_path, w, h):
 
 @needs_exe
 def test_cpp_host_c1_bitexact(tmp_path):
-    g = gold("image_c1_cbox.npz")
+    """The compiled OpenCLApp binding renders the reference application's C1
+    image: the GPU-treelet tree (mcpt_treelet_gpu, scenebuild.cpp:87-95) and the
+    reference kernels over it (image_c1_app.npz)."""
+    g = gold("image_c1_app.npz")
     w, h, depth, frames, att = (int(x) for x in g["meta"])
     out = _run(tmp_path, 2, g["seeds_in"], "--updates", frames)
     assert out["frames_done"] == frames and out["dumped"] == ""  # 16 frames <= attempt: no dump yet
@@ -67,11 +70,14 @@ def test_cpp_host_c1_bitexact(tmp_path):
 @needs_exe
 @pytest.mark.skipif(not refgpu.available(), reason="oracle/_ref not built")
 def test_cpp_host_dump_equals_reference_hdr(tmp_path):
-    g = gold("image_c1_cbox.npz")
+    from . import oracle as O
+    g = gold("image_c1_app.npz")
     w, h, depth, frames, att = (int(x) for x in g["meta"])
     out = _run(tmp_path, 2, g["seeds_in"])  # attempt + 1 = 17 updates, then the dump
     assert out["frames_done"] == att + 1 and os.path.basename(out["dumped"]) == "cbox.obj.hdr"
-    ref_hist, ref_count, ref_seeds = refgpu.render(scenes.cbox(), S.parse_camera(scenes.CBOX_CAM), w, h, depth,
+    data = scenes.cbox()
+    data = data.with_nodes(O.treelet_gpu(data.nodes, rcp_bits=int(g["rcp_bits"]))[1])
+    ref_hist, ref_count, ref_seeds = refgpu.render(data, S.parse_camera(scenes.CBOX_CAM), w, h, depth,
                                                    att + 1, att, g["seeds_in"])
     hist, count, seeds = _state(tmp_path, w, h)
     assert np.array_equal(count, ref_count) and np.array_equal(seeds, ref_seeds)
@@ -103,7 +109,7 @@ def test_cpp_host_checkpoint_resume_bitexact(tmp_path):
     saves the image state (mcpt_download), destroys it, creates a new one and
     restores the saved arrays (mcpt_upload); the render continues to the C1
     golden image bit for bit."""
-    g = gold("image_c1_cbox.npz")
+    g = gold("image_c1_app.npz")
     w, h, depth, frames, att = (int(x) for x in g["meta"])
     out = _run(tmp_path, 2, g["seeds_in"], "--updates", frames, "--resume-at", 7)
     assert out["frames_done"] == frames

@@ -185,15 +185,26 @@ def test_kernel_stripes_follow_dist_owned_rows(rnd):
     dsc.close()
 
 
-def test_app_from_config_json_reproduces_c1(tmp_path):
+@pytest.mark.parametrize("variant", ["", "15"])
+def test_app_from_config_json_reproduces_c1(tmp_path, variant):
     """The reference application loop driven by config.json (configid 2 = C1)
-    reproduces the reference image and dumps <objname>.hdr like ColorOut."""
+    reproduces the reference APPLICATION's image — the reference kernels over
+    the GPU-treelet tree SceneCL renders over (scenebuild.cpp:87-95; golden
+    image_c1_app.npz, tools/make_goldens.py app) — for splitmix seeds and for
+    MSVC rand()'s 15-bit seeds (scenebuild.cpp:116-118, variant "15"), and
+    dumps <objname>.hdr like ColorOut."""
+    import hashlib
+
     from montecarlopathtracing_amd.app import App
-    g = gold("image_c1_cbox.npz")
-    app = App(scenes.CFG, configid=2, seeds=g["seeds_in"], out_dir=str(tmp_path))
+    g = gold("image_c1_app.npz")
+    app = App(scenes.CFG, configid=2, seeds=g["seeds_in" + variant], out_dir=str(tmp_path))
+    app.init()
+    assert hashlib.sha256(app.data.nodes.tobytes()).hexdigest() == str(g["nodes_sha256"])
     app.update(16)                      # frames 0..15 (attempt = 16: all accumulate)
     assert app.dumped is None           # dump happens after attempt + 1 frames
-    assert_bits_equal(app.state.hist.cpu().numpy(), g["hist"], "app hist")
+    assert_bits_equal(app.state.count.cpu().numpy(), g["count" + variant], "app count")
+    assert_bits_equal(app.state.seeds_np(), g["seeds" + variant], "app seeds")
+    assert_bits_equal(app.state.hist.cpu().numpy(), g["hist" + variant], "app hist")
     app.update(1)
     assert app.dumped and os.path.basename(app.dumped) == "cbox.obj.hdr"
     assert open(app.dumped, "rb").read() == S.encode_hdr(app.image())

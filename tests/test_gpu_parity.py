@@ -228,6 +228,24 @@ def test_render_over_treelet_bvh_bitexact(rnd, name, getter, camjson, depth):
     assert_bits_equal(h_, rh, "hist")
 
 
+@needs_ref
+@pytest.mark.parametrize("name,getter,camjson,depth", [("cbox", scenes.cbox, scenes.CBOX_CAM, 6),
+                                                       ("mis", scenes.mis, scenes.MIS_CAM, 12),
+                                                       ("dining", scenes.dining, scenes.DINING_CAM, 8)])
+def test_render_over_gpu_treelet_bvh_bitexact(rnd, name, getter, camjson, depth):
+    """The tree every reference render traverses (TreeletBVH<GPU>,
+    scenebuild.cpp:87-95): the HIP path over mcpt_treelet_gpu_device's tree
+    matches the reference kernels over the same tree bit for bit, per bounce
+    and over whole renders."""
+    data = getter()
+    data = data.with_nodes(R.treelet_gpu_device(data.nodes))
+    _bounce_chain(rnd, data, camjson, 48, 40, 4, L.MODE_EXACT)
+    (h_, c_, s_), (rh, rc, rs) = _render_both(rnd, data, camjson, 64, 64, depth, 6, 4)
+    assert_bits_equal(c_, rc, "count")
+    assert_bits_equal(s_, rs, "seeds")
+    assert_bits_equal(h_, rh, "hist")
+
+
 NEAR_TIES = [("cbox", 0.0, scenes.CBOX_CAM), ("mis", 0.0, scenes.MIS_CAM), ("mis", 3e-6, scenes.MIS_CAM)]
 
 

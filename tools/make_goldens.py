@@ -12,6 +12,7 @@
     python tools/make_goldens.py gpu  OUTDIR
     python tools/make_goldens.py cpu  OUTDIR
     python tools/make_goldens.py bvh  OUTDIR   (GPU box: EPO.cl per triangle)
+    python tools/make_goldens.py app  OUTDIR   (GPU box: C1 over the GPU-treelet tree)
 """
 import ctypes
 import hashlib
@@ -105,6 +106,32 @@ def bvh(out):
         np.savez_compressed(os.path.join(out, "epo_%s.npz" % name), **rec)
 
 
+def app(out):
+    """C1 as the reference APPLICATION renders it: SceneCL restructures a fresh
+    HLBVH with the GPU treelet kernel for every bvhtype (scenebuild.cpp:87-95).
+    The tree is the CPU restatement of treeletBVH.cl (oracle/
+    mcpt_oracle_treelet_gpu.cpp, fed this GPU's v_rcp_f32), the image the
+    reference's own kernels over it (tests/refgpu.py), for the splitmix seeds
+    of image_c1_cbox.npz and MSVC rand()'s 15-bit variant of them."""
+    from tests import oracle as O
+    from tests import refgpu
+    os.makedirs(out, exist_ok=True)
+    data = scenes.cbox()
+    rcp = int(refgpu.rcp_f32(O.root_area_mant(data.nodes))[0].view(np.uint32))
+    rc, nodes, _ = O.treelet_gpu(data.nodes, rcp_bits=rcp)
+    assert rc == 0
+    data = data.with_nodes(nodes)
+    w, h, depth, frames, att = 256, 256, 4, 16, 16
+    rec = {"meta": np.array([w, h, depth, frames, att], np.int32), "rcp_bits": np.uint32(rcp),
+           "nodes_sha256": hashlib.sha256(nodes.tobytes()).hexdigest()}
+    for tag, variant in (("", "splitmix"), ("15", "msvc15")):
+        seeds = R.default_seeds(w * h, variant=variant)
+        hh, cc, ss = refgpu.render(data, S.parse_camera(scenes.CBOX_CAM), w, h, depth, frames, att, seeds)
+        rec.update({"hist" + tag: hh, "count" + tag: cc, "seeds" + tag: ss, "seeds_in" + tag: seeds})
+    np.savez_compressed(os.path.join(out, "image_c1_app.npz"), **rec)
+    print("app golden written to", out)
+
+
 def cpu(out):
     """Reference tinyobj + stb fixtures (oracle/_ref/libref_io.so)."""
     so = ctypes.CDLL(os.path.join(ROOT, "oracle", "_ref", "libref_io.so"))
@@ -139,4 +166,4 @@ def cpu(out):
 
 if __name__ == "__main__":
     mode, out = sys.argv[1], sys.argv[2]
-    {"gpu": gpu, "cpu": cpu, "bvh": bvh}[mode](out)
+    {"gpu": gpu, "cpu": cpu, "bvh": bvh, "app": app}[mode](out)
