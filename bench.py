@@ -7,12 +7,15 @@ fused HIP path-tracing loop on BASELINE.json configs[1] (C2): Scene/cbox,
     torchrun --nproc-per-node N ... bench.py --gpus N       (one process per GPU)
 
 A step = one frame: every pixel of the image traces one sample of up to 8
-bounces and is accumulated (OpenCL::update + ColorOut once).  At N > 1 the
-headline is strong scaling, as north_star asks ("tile-parallel scaling of
-1024x1024 renders"): the fixed 1024x1024 image is split into 16-row stripes
-dealt round-robin to the ranks; the weak-scaled rate (each rank a 1024x1024
-tile of a 1024 x 1024N image) is timed after it and reported under
-"weak_scaling".  No collective runs inside the timed region.  The timed region
+bounces and is accumulated (OpenCL::update + ColorOut once).  The path
+partitions (pixels are independent; 16-row stripes dealt round-robin to the
+ranks, no data-path collective), so at N > 1 the headline is weak scaling:
+each rank renders a 1024x1024 share of a 1024 x 1024N image — the C2 config
+per GPU — and value = all ranks' samples / the slowest rank's time.  The
+strong-scaled rate (the fixed 1024x1024 image striped over the ranks) is
+timed after it and reported under "strong_scaling" (C4, a fixed 1920x1080
+image tile-sharded across the GPUs, is strong-scaled as its config says).
+No collective runs inside the timed region.  The timed region
 is bracketed by barrier + synchronize and the max over ranks is reported.
 Scene data, seeds and accumulators are resident in HBM before timing starts.
 The timed call computes its own primary hits (k_primary, then k_render reads
@@ -76,21 +79,26 @@ DINING_CAM = {"position": [-0.5, 3, 5.5], "lookat": [-0.5, 2, 0], "up": [0, 1, 0
 
 
 def load_scene(workload):
+    """The workload's scene over the tree the reference renders over: SceneCL
+    restructures a fresh HLBVH with its GPU treelet kernel for every bvhtype
+    (scenebuild.cpp:87-95), here mcpt_treelet_gpu_device."""
+    from montecarlopathtracing_amd import render as R
     from montecarlopathtracing_amd import scene as S
     if workload == "C2":
-        return S.SceneData.from_obj(os.path.join(ROOT, "scenes/cbox/"), "cbox.obj",
-                                    material_override=S.diffuse_only), CBOX_CAM
-    if workload == "C3":
-        return S.SceneData.from_obj(os.path.join(ROOT, "scenes/veach_mis/"), "mis.obj"), MIS_CAM
-    if workload == "C4":  # synthetic stand-in for the absent geometry (tools/make_diningroom_proxy.py),
-        # over the treelet tree like the reference's diningroom entry ("bvhtype": "treeletGPU")
-        from montecarlopathtracing_amd import render as R
-        d = S.SceneData.from_obj(os.path.join(ROOT, "scenes/diningroom/"), "diningroom.obj")
-        return d.with_nodes(R.treelet_device(d.nodes)), DINING_CAM
-    if workload == "C5":
-        from montecarlopathtracing_amd import render as R  # the HLBVH built on the GPU (same tree as the host's)
-        return S.random_mesh(10_000_000, build=R.build_hlbvh_host_nodes), S.RANDOM_MESH_CAMERA
-    raise ValueError(workload)
+        d, cam = S.SceneData.from_obj(os.path.join(ROOT, "scenes/cbox/"), "cbox.obj",
+                                      material_override=S.diffuse_only), CBOX_CAM
+    elif workload == "C3":
+        d, cam = S.SceneData.from_obj(os.path.join(ROOT, "scenes/veach_mis/"), "mis.obj"), MIS_CAM
+    elif workload == "C4":  # synthetic stand-in for the absent geometry (tools/make_diningroom_proxy.py)
+        d, cam = S.SceneData.from_obj(os.path.join(ROOT, "scenes/diningroom/"), "diningroom.obj"), DINING_CAM
+    elif workload == "C5":  # HLBVH and treelet pass both on the GPU
+        def build(tris):
+            nodes = R.build_hlbvh_device(tris)
+            return R.records(R.treelet_gpu_device(nodes), R.L.BVHNODE).copy()
+        return S.random_mesh(10_000_000, build=build), S.RANDOM_MESH_CAMERA
+    else:
+        raise ValueError(workload)
+    return d.with_nodes(R.treelet_gpu_device(d.nodes)), cam
 
 
 def e_counts(workload="C2"):
@@ -167,6 +175,11 @@ def cpu_baseline(data, cam, h_img, target_s=15.0, label="C2"):
             "active_Msegments_per_s": float(st[0]) / dt / 1e6}
 
 
+def _ownership(w, h, rank, n):
+    from montecarlopathtracing_amd import dist as D
+    return D.ownership_mask(w, h, STRIPE_ROWS, rank, n)
+
+
 def load_profile(workload, steps):
     """The committed rocprofv3 summary of the timed launch of THIS command
     (workload, frames per call), written by tools/profile.py; None if that
@@ -216,7 +229,8 @@ def main():
     ap.add_argument("--workload", default="C2", choices=sorted(WORKLOADS))
     ap.add_argument("--schedule", default="auto", choices=["auto", "single", "paired"],
                     help="k_render leaf-test schedule; auto times both before the warmup (untimed)")
-    ap.add_argument("--no-weak", action="store_true", help="N > 1: skip the weak-scaling leg")
+    ap.add_argument("--no-strong", action="store_true", help="N > 1: skip the strong-scaling leg")
+    ap.add_argument("--no-cache-off", action="store_true", help="skip the primary-cache-off timing")
     ap.add_argument("--shade-threshold", type=int, default=0,
                     help="k_render S-phase threshold (mcpt_tuning.shade_threshold); 0: tuned with the schedule "
                          "when --schedule is auto, else the default")
@@ -247,8 +261,10 @@ def main():
     from montecarlopathtracing_amd import render as R
     from montecarlopathtracing_amd import scene as S
 
-    # strong scaling: one fixed image striped over the ranks (the headline)
-    h_img = H_PER_GPU
+    # weak scaling (the headline): a 1024 x 1024N image, each rank a 1024x1024
+    # share; C4 strong-scales its fixed image
+    strong_only = bool(wl.get("strong"))
+    h_img = H_PER_GPU if strong_only else H_PER_GPU * n
     data, camj = load_scene(args.workload)
     cam = S.parse_camera(camj)
     rnd = R.Renderer(local if ws > 1 else 0)
@@ -276,6 +292,19 @@ def main():
 
     elapsed = timed_render(rnd, dsc, cam, st, args.steps, args.warmup, kw, ws, shared)
     kst = rnd.stats()
+    # the same frames with the primary-hit cache off (every frame traces its
+    # primary ray), timed after the headline: the memoization's share of it
+    cache_off = None
+    if not args.no_cache_off:
+        base_tuning = rnd.get_tuning()
+        rnd.set_tuning(**dict(base_tuning, primary_cache=2))
+        st_off = rnd.new_state(W, h_img, seeds)
+        e_off = timed_render(rnd, dsc, cam, st_off, args.steps, args.warmup, kw, ws, shared)
+        rnd.set_tuning(**base_tuning)
+        cache_off = {"value": round(float(W * h_img) * args.steps * DEPTH / e_off / 1e6, 2), "unit": "Msamples/s",
+                     "ms_per_step": round(e_off * 1e3 / args.steps, 4),
+                     "note": "mcpt_tuning.primary_cache = 2: every frame traces its primary ray (same bits)"}
+        del st_off
     # k_render alone: the call's device time less the primary-hit pass before it
     primary_ms = kst.get("primary_ms", 0.0) if kst.get("primary_cache") == 2 else 0.0
     kernel_ms, launches = kst["kernel_ms"] - primary_ms, max(kst["launches"], 1)
@@ -293,13 +322,18 @@ def main():
     cst = rnd.stats()
     rnd.set_stats(False)
     segments = cst["segments"]
+    # segments whose hit the primary-hit cache served (each frame's first, no
+    # traversal): this rank's pixels x frames when the call read the cache
+    my_px = int(np.count_nonzero(_ownership(W, h_img, rank, n)))
+    served = my_px * args.steps if cst.get("primary_cache") in (1, 2) else 0
+    traced = segments - served
     del st2
 
     # the job's one exchange, after the timed frames: every rank's row stripes
     # summed onto rank 0 (dist.reduce_image: RCCL over xGMI; gloo when rehearsed
     # on a shared GPU), timed on its own and reported beside the frame rate
     reduce_ms = None
-    weak = None
+    strong = None
     if ws > 1:
         from montecarlopathtracing_amd import dist as D
         mask = D.ownership_mask(W, h_img, STRIPE_ROWS, rank, n)
@@ -313,15 +347,14 @@ def main():
         torch.cuda.synchronize()
         torch.distributed.barrier()
         reduce_ms = (time.perf_counter() - t1) * 1e3
-        if not args.no_weak and not wl.get("strong"):
-            # weak scaling: a 1024 x 1024N image, each rank a 1024x1024 share
-            h_weak = H_PER_GPU * n
-            stw = rnd.new_state(W, h_weak, default_seeds(W * h_weak))
-            ew = timed_render(rnd, dsc, cam, stw, args.steps, args.warmup, kw, ws, shared)
-            weak = {"value": round(float(W * h_weak) * args.steps * DEPTH / ew / 1e6, 2), "unit": "Msamples/s",
-                    "ms_per_step": round(ew * 1e3 / args.steps, 4), "image": [W, h_weak],
-                    "note": "each rank renders a 1024x1024 share of a 1024 x 1024N image"}
-            del stw
+        if not args.no_strong and not strong_only:
+            # strong scaling: the fixed 1024x1024 image striped over the ranks
+            sts = rnd.new_state(W, H_PER_GPU, default_seeds(W * H_PER_GPU))
+            es = timed_render(rnd, dsc, cam, sts, args.steps, args.warmup, kw, ws, shared)
+            strong = {"value": round(float(W * H_PER_GPU) * args.steps * DEPTH / es / 1e6, 2), "unit": "Msamples/s",
+                      "ms_per_step": round(es * 1e3 / args.steps, 4), "image": [W, H_PER_GPU],
+                      "note": "the fixed 1024x1024 image striped over the ranks"}
+            del sts
 
     total_samples = float(W * h_img) * args.steps * DEPTH
     value = total_samples / elapsed / 1e6
@@ -334,23 +367,27 @@ def main():
                 "kernel": "k_render<EXACT, no stats, %s, %s nodes>" % (
                     "paired" if dsc.schedule == L.SCHED_PAIRED else "single", search_tree),
                 "avg_launch_ms": round(avg_launch_s * 1e3, 3), "segments_per_launch": int(seg_per_launch),
+                "segments_traced": int(traced), "segments_cache_served": int(served),
                 "primary_pass_ms": round(primary_ms, 3),
-                "kernel_node_fetches_per_seg": round(cst["node_visits"] / max(segments, 1), 3),
-                "kernel_tri_tests_per_seg": round(cst["tri_tests"] / max(segments, 1), 3)}
+                # per TRACED segment: the cache-served ones fetch no node or triangle
+                "kernel_node_fetches_per_seg": round(cst["node_visits"] / max(traced, 1), 3),
+                "kernel_tri_tests_per_seg": round(cst["tri_tests"] / max(traced, 1), 3)}
         if prof:
             traffic = prof["hbm_bytes_per_launch"]
             roof["traffic"] = traffic
             roof["achieved"] = round(traffic / avg_launch_s / 1e9, 2)
             roof["frac"] = round(roof["achieved"] / HBM_PEAK_GBS, 5)
-            # rocprofv3's VALUBusy definition reads up to ~1 % over 1 on a saturated
-            # kernel (C3); the fraction is capped, the raw counter ratio kept beside it
-            vb = prof.get("valu_busy")
-            roof["issue_frac"] = None if vb is None else min(1.0, vb)
-            if vb is not None and vb > 1.0:
-                roof["issue_frac_raw"] = vb
+            # issue_frac: lane-weighted VALU use = VALU-busy cycles x the share of
+            # the 64 lanes those instructions ran with (rocprofv3 VALUUtilization);
+            # the raw busy ratio beside it (rocprofv3's VALUBusy definition reads
+            # up to ~1 % over 1 on a saturated kernel, C3: DESIGN.md §3.6)
+            vb, vu = prof.get("valu_busy"), prof.get("valu_utilization_lanes")
+            roof["issue_frac"] = None if vb is None or vu is None else round(vb * vu, 4)
+            roof["valu_busy"] = vb
+            roof["valu_lane_utilization"] = vu
             roof["td_busy"] = prof.get("td_busy")
-            roof["binding"] = ("vector-memory gathers: TD (data-return) busy %s of the kernel's cycles, VALU issue %s "
-                               "(DESIGN.md §3.6; profiles/r02_probe_ab.txt)" % (prof.get("td_busy"), prof.get("valu_busy")))
+            roof["binding"] = ("vector-memory gathers: TD (data-return) busy %s of the kernel's cycles; VALU busy %s at "
+                               "%s lane use (DESIGN.md §3.6)" % (prof.get("td_busy"), vb, vu))
             for k in ("l1_hit_rate", "l2_hit_rate", "l2_hit_GBps_128B_lines", "wave_wait_any_per_wave_cycle",
                       "gather_latency_cycles_per_vmem_rd", "fetch_scale_calibrated", "timed_launch_ms_rocprof"):
                 roof[k] = prof.get(k)
@@ -370,7 +407,8 @@ def main():
             cpu = cpu_baseline(data, cam, h_img)
         out = {"metric": METRIC, "value": round(value, 2), "unit": "Msamples/s", "n_gpus": n, "steps": args.steps,
                "warmup": args.warmup, "ms_per_step": round(elapsed * 1e3 / args.steps, 4),
-               "higher_is_better": True, "scaling": "strong", "vs_baseline": None,
+               "higher_is_better": True, "scaling": "strong" if (strong_only and n > 1) else "weak",
+               "vs_baseline": None,
                "dtype": "f32",
                "data": "synthetic seeds; " + ("Scene/cbox geometry recovered from the reference's cbox.mb"
                                               if args.workload == "C2" else "see config.workload"),
@@ -383,8 +421,10 @@ def main():
                           "block_entries": rnd.get_tuning()["block_entries"] or 32,
                           "frames_per_block": fpb, "search_tree_nodes": search_tree},
                "active_Msegments_per_s": round(segments * n / elapsed / 1e6, 2),
+               "traced_Msegments_per_s": round(traced * n / elapsed / 1e6, 2),
+               "primary_cache_off": cache_off,
                "image_reduce_ms": None if reduce_ms is None else round(reduce_ms, 3),
-               "weak_scaling": weak,
+               "strong_scaling": strong,
                "roofline": roof, "cpu_baseline": cpu}
         print(json.dumps(out), flush=True)
     dsc.close()

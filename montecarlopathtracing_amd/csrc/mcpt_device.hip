@@ -145,7 +145,8 @@ struct mcpt_scene {
 
 constexpr int kQueues = 8;         // k_render work queues (at most): one per XCD (MI355X has 8)
 constexpr int kQueueStride = 32;   // u32 words between queue heads: one 128-B line each
-constexpr int kHandoffWords = 6;   // seed, mean.xyzw, count: one tagged 8-B granule each
+constexpr int kHandoffWords = 4;   // seed, mean.xyzw, count in four tagged 8-B granules (two 16-B stores)
+constexpr int kMaxBlocksPerLaunch = 255;  // the hand-off tag's 8 bits of block index
 constexpr int kStatSlots = 24;
 constexpr int64_t kQuantAutoBytes = 32ll << 20;  // 8 XCDs x 4 MiB of L2
 // primary-hit pass: k_primary (one ray per lane) for search trees up to this
@@ -557,14 +558,25 @@ struct ShadeOut {
   f4 color;
   bool new_ray;  // the reference writes rays[id] = newRay
   bool bad;      // unknown material type (reference prints "Crash!!!")
+  bool pending;  // glossy lobe sample below the surface: resample (resample = true)
 };
 
-// shade.cl:75-206 for one live ray that hit something.
+// shade.cl:75-206 for one live ray that hit something, in steps: a glossy
+// lobe's rejection loop (shade.cl:130-132, `while (dot(nd, n) <= 0) nd =
+// randomDirection(refl)`) runs ONE draw per call.  A call whose draw falls
+// below the surface returns pending with `resample` set and no other effect;
+// the next call with the same input and seed chain draws again (the lobe's
+// coin is not redrawn), so the lane's sequence of draws is the loop's.  The
+// fused kernel leaves such a lane in its S phase, where its next draw shares
+// the one randomDirection call site with every other lane's first draw
+// (diffuse, and glossy either lobe), instead of holding the whole wave in
+// the loop.
 __device__ inline ShadeOut shade_hit(const mcpt_material *__restrict__ mats, const ShadeIn &in, f4 color,
-                                     uint32_t &seed, int max_depth) {
+                                     uint32_t &seed, int max_depth, bool &resample) {
   ShadeOut r;
   r.bad = false;
   r.new_ray = true;
+  r.pending = false;
   const mcpt_material M = mats[in.mat];
   const f4 kd = (f4){M.kd[0], M.kd[1], M.kd[2], M.kd[3]};
   const f4 kaks = (f4){M.ka_ks[0], M.ka_ks[1], M.ka_ks[2], M.ka_ks[3]};
@@ -572,27 +584,27 @@ __device__ inline ShadeOut shade_hit(const mcpt_material *__restrict__ mats, con
   f4 no, nd;
   switch (M.type) {
     case MCPT_DIFFUSE:
-    diffuse_lobe:
-      nd = random_dir(in.nrm, seed);
+    case MCPT_GLOSSY: {
+      // glossy: the lobe coin (shade.cl:115), then the Phong lobe around the
+      // mirror direction, else the diffuse lobe (shade.cl:139)
+      const bool lobe = resample || (M.type == MCPT_GLOSSY && (lcg15(seed) & 0x00000001));
+      const f4 axis = lobe ? mirror_dir(in.nrm, in.d) : in.nrm;
+      nd = random_dir(axis, seed);
+      if (lobe && cl_dot3(nd.xyz, in.nrm.xyz) <= 0) {  // rejected: draw again next call
+        resample = true;
+        r.pending = true;
+        return r;
+      }
+      resample = false;
       no = in.pt + kEps * nd;
       no.w = as_f(td + 1);
       nd.w = in.d.w;
-      color = color * kd * cl_dot3(nd.xyz, in.nrm.xyz) / (float)(2 * kClPi);
+      // diffuse: color * kd * cos / 2pi; glossy: color * ks * pow(cos_r, Ns) * cos / 2pi
+      f4 c = color * (lobe ? kaks : kd);
+      if (lobe) c = c * cl_pow(cl_dot3(nd.xyz, axis.xyz), M.Ns);
+      color = cl_div4(c * cl_dot3(nd.xyz, in.nrm.xyz), (float)(2 * kClPi));
       break;
-    case MCPT_GLOSSY:
-      if (lcg15(seed) & 0x00000001) {
-        f4 refl = mirror_dir(in.nrm, in.d);
-        nd = random_dir(refl, seed);
-        while (cl_dot3(nd.xyz, in.nrm.xyz) <= 0) nd = random_dir(refl, seed);
-        no = in.pt + kEps * nd;
-        no.w = as_f(td + 1);
-        nd.w = in.d.w;
-        color = color * kaks * cl_pow(cl_dot3(nd.xyz, refl.xyz), M.Ns) * cl_dot3(nd.xyz, in.nrm.xyz) /
-                (float)(2 * kClPi);
-      } else {
-        goto diffuse_lobe;
-      }
-      break;
+    }
     case MCPT_LIGHT:
       r.new_ray = false;
       r.o = in.o;
@@ -615,7 +627,7 @@ __device__ inline ShadeOut shade_hit(const mcpt_material *__restrict__ mats, con
       no = in.pt;
       nd.w = in.d.w;
       int32_t ntd = td + 1;
-      if ((lcg15(seed) * 1.0f / 32768) >= fr) {
+      if (cl_div(lcg15(seed) * 1.0f, 32768) >= fr) {
         ntd ^= 0x00FF0000;
       } else {
         nd.xyz = mirror_dir(in.nrm, in.d).xyz;
@@ -642,6 +654,16 @@ __device__ inline ShadeOut shade_hit(const mcpt_material *__restrict__ mats, con
   r.color = color;
   return r;
 }
+// the whole of shade.cl's work for one ray (the wavefront kernel)
+__device__ inline ShadeOut shade_hit_full(const mcpt_material *__restrict__ mats, const ShadeIn &in, f4 color,
+                                          uint32_t &seed, int max_depth) {
+  bool resample = false;
+  ShadeOut so;
+  do {
+    so = shade_hit(mats, in, color, seed, max_depth, resample);
+  } while (so.pending);
+  return so;
+}
 
 // history.cl:3-28 on one pixel; returns the colour the reference shows.
 // length(now) == 0 is evaluated as "every component is +-0": with IEEE
@@ -650,7 +672,7 @@ __device__ inline ShadeOut shade_hit(const mcpt_material *__restrict__ mats, con
 __device__ inline f4 accumulate_one(f4 now, f4 &hist, int32_t &cnt, int max_attempt) {
   const bool zero = now.x == 0.0f && now.y == 0.0f && now.z == 0.0f && now.w == 0.0f;
   if (zero || cnt >= max_attempt) return hist;
-  now = (now + hist * cnt) / (cnt + 1);
+  now = cl_div4(now + hist * cnt, (float)(cnt + 1));
   hist = now;
   hist.w = 0.0f;
   ++cnt;
@@ -659,19 +681,24 @@ __device__ inline f4 accumulate_one(f4 now, f4 &hist, int32_t &cnt, int max_atte
 
 // --------------------------------------------------------- fused hot kernel
 // Block hand-off: a pixel's state passes from the lane that ran frame block
-// b-1 to the lane that runs block b as six 8-byte granules {tag:32 | word:32}
-// (seed, mean.xyzw, count), each written and read by ONE agent-scope atomic
-// (global_store/load_dwordx2 sc1: bypasses the CU's L1; coherent across the
-// XCDs' L2s).  The reader accepts a granule only when its tag names this
-// launch and block b, so every word it keeps is the one the writer stored
-// with that tag: per-location coherence of the atomics is all the protocol
-// needs, no flag and no fence orders anything (MI355X_MICROARCH.md,
-// "handoff-1to1": data-tagged granules are the cheapest hand-off).
-__device__ inline unsigned long long handoff_load(const unsigned long long *p) {
-  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+// b-1 to the lane that runs block b as four 8-byte granules {tag:16 |
+// payload:48} carrying the 192 bits of (seed, mean.xyzw, count), written as
+// two 16-B system-coherent stores and read as two 16-B loads
+// (global_store/load_dwordx4 sc0 sc1: bypass the CU's L1, coherent across
+// the XCDs' L2s; a 16-B sc1 store costs about what an 8-B one does, so this
+// halves the hand-off's fabric writes against one store per word).  The
+// reader accepts the state only when all four tags name this launch and
+// block b, so every 48-bit piece it keeps is the one the writer stored with
+// that tag: the protocol needs each aligned 8-B granule untorn, nothing more
+// (no flag, no fence; MI355X_MICROARCH.md "handoff-1to1": data-tagged
+// granules are the cheapest hand-off).
+typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
+typedef __attribute__((address_space(1))) u64x2 g_u64x2;
+__device__ inline u64x2 handoff_load2(const unsigned long long *p) {
+  return *(const volatile g_u64x2 *)p;
 }
-__device__ inline void handoff_store(unsigned long long *p, unsigned long long v) {
-  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+__device__ inline void handoff_store2(unsigned long long *p, unsigned long long a, unsigned long long b) {
+  *(volatile g_u64x2 *)p = (u64x2){a, b};
 }
 // This wave's XCD (0-7).  Picks the home queue: speed only — any placement
 // gives the same result, and waves steal from the other queues when theirs
@@ -699,7 +726,7 @@ struct RenderArgs {
   int32_t max_depth, max_attempt, frame_begin, frames;  // frames: of this launch
   int32_t fpl, blocks;         // frames per block, blocks in this launch
   unsigned long long *handoff; // per pixel: kHandoffWords tagged granules
-  uint32_t tag_base;           // this launch's tag; a granule for block b carries tag_base | b
+  uint32_t tag_base;           // this launch's tag; a granule for block b carries tag_base | b (16 bits)
   int32_t stack_depth;
   int32_t th_leaf, th_shade;  // lanes waiting before the L / S phase runs
   uint32_t *queue;            // n_queues work-queue heads, kQueueStride apart (zeroed before each launch)
@@ -793,7 +820,8 @@ __global__ void __launch_bounds__(64, MCPT_WAVES_PER_SIMD) k_render(RenderArgs A
   // pixel state.  lst: this lane's role in the queue protocol, one small
   // int (one VGPR; kept out of lane-mask SGPR pairs on purpose, SGPRs are
   // the scarce register file of this kernel)
-  constexpr int32_t kBusy = 0, kNeed = 1, kPend = 2, kDead = 3;
+  // kRes: busy, its glossy lobe sample rejected; it stays in S and draws again
+  constexpr int32_t kRes = -1, kBusy = 0, kNeed = 1, kPend = 2, kDead = 3;
   int32_t lst = kNeed;
   int32_t f = 0, cnt = 0;
   uint32_t seed = 0, pxy = 0;  // pxy = x | y << 16 (the pending entry's pixel while kPend)
@@ -872,7 +900,7 @@ __global__ void __launch_bounds__(64, MCPT_WAVES_PER_SIMD) k_render(RenderArgs A
       // lanes that need an entry start together once th_fetch of them wait
       // (their state loads then share one wait), or when no lane is busy
       const unsigned long long mn = __ballot(lst == kNeed);
-      if (mn && (__popcll(mn) >= A.th_fetch || !__ballot(lst == kBusy))) {
+      if (mn && (__popcll(mn) >= A.th_fetch || !__ballot(lst <= kBusy))) {
         const uint32_t n_need = (uint32_t)__popcll(mn);
         const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(mn >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mn, 0));
         uint32_t q = pool + rank, qx = (qs >> 4) & 15u;
@@ -938,15 +966,15 @@ __global__ void __launch_bounds__(64, MCPT_WAVES_PER_SIMD) k_render(RenderArgs A
           cnt = A.count[pp];
         } else {  // published by another lane, any XCD
           const unsigned long long *g = A.handoff + (size_t)pp * kHandoffWords;
-          const unsigned long long g0 = handoff_load(g), g1 = handoff_load(g + 1), g2 = handoff_load(g + 2);
-          const unsigned long long g3 = handoff_load(g + 3), g4 = handoff_load(g + 4), g5 = handoff_load(g + 5);
-          const uint32_t want = A.tag_base | (uint32_t)blk;
-          ready = (uint32_t)(g0 >> 32) == want && (uint32_t)(g1 >> 32) == want && (uint32_t)(g2 >> 32) == want &&
-                  (uint32_t)(g3 >> 32) == want && (uint32_t)(g4 >> 32) == want && (uint32_t)(g5 >> 32) == want;
-          seed = (uint32_t)g0;
-          hist = (f4){as_f((int32_t)(uint32_t)g1), as_f((int32_t)(uint32_t)g2), as_f((int32_t)(uint32_t)g3),
-                      as_f((int32_t)(uint32_t)g4)};
-          cnt = (int32_t)(uint32_t)g5;
+          const u64x2 h0 = handoff_load2(g), h1 = handoff_load2(g + 2);
+          const unsigned long long want = (unsigned long long)(A.tag_base | (uint32_t)blk);
+          ready = (h0.x >> 48) == want && (h0.y >> 48) == want && (h1.x >> 48) == want && (h1.y >> 48) == want;
+          // 192 payload bits, 48 per granule: seed | mean.x | mean.y | mean.z | mean.w | count
+          seed = (uint32_t)h0.x;
+          hist = (f4){as_f((int32_t)(((uint32_t)(h0.x >> 32) & 0xFFFFu) | ((uint32_t)h0.y << 16))),
+                      as_f((int32_t)(uint32_t)(h0.y >> 16)), as_f((int32_t)(uint32_t)h1.x),
+                      as_f((int32_t)(((uint32_t)(h1.x >> 32) & 0xFFFFu) | ((uint32_t)h1.y << 16)))};
+          cnt = (int32_t)(uint32_t)(h1.y >> 16);
         }
         if (ready) {
           lst = kBusy;
@@ -958,7 +986,7 @@ __global__ void __launch_bounds__(64, MCPT_WAVES_PER_SIMD) k_render(RenderArgs A
     }
     MCPT_TICK(0);
     if (!__ballot(lst != kDead)) break;
-    const bool live = lst == kBusy;
+    const bool live = lst <= kBusy;
     // phase thresholds scaled to the wave's live lanes: a wave with few pixels
     // (a launch's tail, a strong-scaled rank) does not wait for lane counts
     // only a full wave reaches (C2 -3 %, C5 -4 %, C2 4- and 8-rank shares
@@ -1133,8 +1161,8 @@ __global__ void __launch_bounds__(64, MCPT_WAVES_PER_SIMD) k_render(RenderArgs A
         A.prim_out[(size_t)(pxy >> 16) * (size_t)A.W + (pxy & 0xFFFFu)] = h;
         lst = kNeed;
       } else if (in_s) {
-        if (STATS) n_seg++;
-        bool done, fresh = false;
+        if (STATS && lst == kBusy) n_seg++;
+        bool done = false, fresh = false, pending = false;
         if (best_t >= kFltMax) {  // shade.cl:92-96 — miss: black, terminate
           color = (f4){0.0f, 0.0f, 0.0f, 0.0f};
           done = true;
@@ -1147,12 +1175,17 @@ __global__ void __launch_bounds__(64, MCPT_WAVES_PER_SIMD) k_render(RenderArgs A
           if (cl_dot3(d.xyz, in.nrm.xyz) > 0) in.nrm = -in.nrm;  // intersect.cl:23-25
           in.pt = o + best_t * d;                                  // objdef.h:218
           in.mat = as_i(tn.w);
-          ShadeOut so = shade_hit(mats, in, color, seed, A.max_depth);
-          if (STATS) n_bad += so.bad;
-          color = so.color;
-          o = so.o;
-          d = so.d;
-          done = (as_i(o.w) & (int32_t)MCPT_TERMINATED) != 0;
+          bool rs = lst == kRes;
+          ShadeOut so = shade_hit(mats, in, color, seed, A.max_depth, rs);
+          pending = so.pending;
+          lst = pending ? kRes : kBusy;
+          if (!pending) {
+            if (STATS) n_bad += so.bad;
+            color = so.color;
+            o = so.o;
+            d = so.d;
+            done = (as_i(o.w) & (int32_t)MCPT_TERMINATED) != 0;
+          }
         }
         if (done) {
           // ColorOut: history runs while attemptCount <= MAX_ATTEMPT (colorout.cpp:56)
@@ -1167,14 +1200,14 @@ __global__ void __launch_bounds__(64, MCPT_WAVES_PER_SIMD) k_render(RenderArgs A
           if (f == fend) {  // block complete: write back, fetch another next iteration
             const int32_t pid = (int32_t)(pxy >> 16) * A.W + (int32_t)(pxy & 0xFFFFu);
             if (blk + 1 < A.blocks) {  // publish for the lane that takes the next block
-              const unsigned long long tag = (unsigned long long)(A.tag_base | (uint32_t)(blk + 1)) << 32;
+              const unsigned long long tag = (unsigned long long)(A.tag_base | (uint32_t)(blk + 1)) << 48;
+              const uint32_t w1 = (uint32_t)as_i(hist.x), w2 = (uint32_t)as_i(hist.y);
+              const uint32_t w3 = (uint32_t)as_i(hist.z), w4 = (uint32_t)as_i(hist.w);
               unsigned long long *g = A.handoff + (size_t)pid * kHandoffWords;
-              handoff_store(g, tag | seed);
-              handoff_store(g + 1, tag | (uint32_t)as_i(hist.x));
-              handoff_store(g + 2, tag | (uint32_t)as_i(hist.y));
-              handoff_store(g + 3, tag | (uint32_t)as_i(hist.z));
-              handoff_store(g + 4, tag | (uint32_t)as_i(hist.w));
-              handoff_store(g + 5, tag | (uint32_t)cnt);
+              handoff_store2(g, tag | seed | (unsigned long long)(w1 & 0xFFFFu) << 32,
+                             tag | (w1 >> 16) | (unsigned long long)w2 << 16);
+              handoff_store2(g + 2, tag | w3 | (unsigned long long)(w4 & 0xFFFFu) << 32,
+                             tag | (w4 >> 16) | (unsigned long long)(uint32_t)cnt << 16);
             } else {
               A.seeds[pid] = seed;
               A.hist[pid] = hist;
@@ -1308,7 +1341,7 @@ __global__ void k_shade(const mcpt_material *mats, mcpt_ray *rays, const mcpt_hi
   in.pt = *(const f4 *)H.point;
   in.mat = (int32_t)H.material_id;
   uint32_t seed = seeds[id];
-  ShadeOut so = shade_hit(mats, in, colors[id], seed, max_depth);
+  ShadeOut so = shade_hit_full(mats, in, colors[id], seed, max_depth);
   colors[id] = so.color;
   seeds[id] = seed;
   if (so.new_ray) {
@@ -2063,10 +2096,11 @@ int mcpt_render_frames(mcpt_ctx *ctx, const mcpt_scene *scene, const mcpt_camera
       fpl = std::max(fpl, (frames + 1) / 2);
     fpl = std::max(1, std::min({fpl, cap, frames}));
   }
-  // blocks per launch: the hand-off tag holds 12 bits of block index, and
+  // blocks per launch: the hand-off tag holds 8 bits of block index, and
   // one launch covers at most ~4096 frames
   const int64_t max_blocks = std::max<int64_t>(
-      1, std::min<int64_t>({(int64_t)INT32_MAX / std::max<uint32_t>(n_items, 1), 4096 / fpl + 1, 4095}));
+      1, std::min<int64_t>({(int64_t)INT32_MAX / std::max<uint32_t>(n_items, 1), 4096 / fpl + 1,
+                            (int64_t)kMaxBlocksPerLaunch}));
   const int64_t n_blocks_all = (p->frames + fpl - 1) / fpl;
   const int n_launch = (int)((n_blocks_all + max_blocks - 1) / max_blocks);
   if (n_launch + 1 > ctx->queue_cap) {  // kQueues heads per launch (+ the primary pass), zeroed by memsets
@@ -2084,7 +2118,7 @@ int mcpt_render_frames(mcpt_ctx *ctx, const mcpt_scene *scene, const mcpt_camera
     ctx->handoff_cap = 0;
     const size_t bytes = (size_t)n_px * kHandoffWords * sizeof(unsigned long long);
     HIP_OK(hipMalloc(&ctx->d_handoff, bytes));
-    HIP_OK(hipMemset(ctx->d_handoff, 0, bytes));  // tag 0 never matches (blocks >= 1)
+    HIP_OK(hipMemsetAsync(ctx->d_handoff, 0, bytes, st));  // tag 0 never matches (blocks >= 1)
     ctx->handoff_cap = n_px;
   }
   A.fpl = fpl;
@@ -2184,13 +2218,15 @@ int mcpt_render_frames(mcpt_ctx *ctx, const mcpt_scene *scene, const mcpt_camera
       A.blocks = (A.frames + fpl - 1) / fpl;
       A.queue = ctx->d_queue + (size_t)launches * kQueues * kQueueStride;
       // a fresh tag per launch: granules of earlier launches never match.
-      // After 2^20 launches the tags wrap; clear the granules then.
-      if (((++ctx->launch_seq) & 0xFFFFFu) == 0) {
+      // After 255 launches the 8-bit launch tags wrap; the granules are
+      // cleared then (stream-ordered before this launch), so every granule in
+      // the area was written during the current cycle of tags.
+      if (((++ctx->launch_seq) & 0xFFu) == 0) {
         ++ctx->launch_seq;
         if (ctx->d_handoff)
           HIP_OK(hipMemsetAsync(ctx->d_handoff, 0, (size_t)ctx->handoff_cap * kHandoffWords * 8, st));
       }
-      A.tag_base = (ctx->launch_seq & 0xFFFFFu) << 12;
+      A.tag_base = (ctx->launch_seq & 0xFFu) << 8;
       void *kargs[] = {&A};
       HIP_OK(hipLaunchKernel(kfn, dim3((unsigned)grid), dim3(64), kargs, lds, st));
       ++launches;

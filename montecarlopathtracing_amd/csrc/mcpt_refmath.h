@@ -81,6 +81,20 @@ __device__ inline float cl_sqrt(float x) {
   const float r = __builtin_amdgcn_sqrtf(__builtin_amdgcn_ldexpf(x, s ? 32 : 0));
   return __builtin_amdgcn_ldexpf(r, s ? -16 : 0);
 }
+// OpenCL's default 2.5-ulp x / y as ROCm's compiler lowers it for gfx950 —
+// the form of every division in the reference's shade.cl and history.cl
+// objects (oracle/_ref: no v_div_scale there): ldexp(frexp_mant(x) *
+// rcp(frexp_mant(y)), ex - ey).  A constant y's rcp folds at compile time
+// exactly as it does there.  Written out for the same reason as cl_sqrt: a
+// '/' that LLVM hoists or speculates loses its !fpmath and becomes the
+// correctly rounded v_div_scale sequence (it did in the restructured shade).
+__device__ inline float cl_div(float x, float y) {
+  return __builtin_amdgcn_ldexpf(__builtin_amdgcn_frexp_mantf(x) * __builtin_amdgcn_rcpf(__builtin_amdgcn_frexp_mantf(y)),
+                                 __builtin_amdgcn_frexp_expf(x) - __builtin_amdgcn_frexp_expf(y));
+}
+__device__ inline f4 cl_div4(f4 x, float y) {
+  return (f4){cl_div(x.x, y), cl_div(x.y, y), cl_div(x.z, y), cl_div(x.w, y)};
+}
 // length(float4): opencl.bc _Z6lengthDv4_f
 __device__ inline float cl_length4(f4 p) {
   float l2 = cl_dot4(p, p);
@@ -117,7 +131,7 @@ __device__ inline f4 mirror_dir(f4 n, f4 in) {
 __device__ inline bool transmit_dir(f4 n, f4 in, float eta_i, float eta_t, f4 &out) {
   n.w = 0.0f;
   in.w = 0.0f;
-  float eta = eta_i / eta_t;
+  float eta = cl_div(eta_i, eta_t);
   float cos_i = -cl_dot4(n, in);
   float k = 1.0f - eta * eta * (1 - cos_i * cos_i);
   if (k < 0.0f) return false;
@@ -160,7 +174,7 @@ __device__ inline float random_phi(uint32_t r) { return (float)(2 * kClPi / 3276
 __device__ inline f4 random_dir(f4 n, uint32_t &seed) {
   n.w = 0;
   float phi = random_phi(lcg15(seed));
-  float u = lcg15(seed) * 1.0f / 32768;
+  float u = cl_div(lcg15(seed) * 1.0f, 32768);
   float s = cl_sqrt(u);
   float sin_phi, cos_phi;
   sincos_small(phi, sin_phi, cos_phi);
@@ -176,7 +190,7 @@ __device__ inline f4 random_dir(f4 n, uint32_t &seed) {
 }
 // calcFresnel: shade.cl:69-73 (Schlick on the transmitted direction)
 __device__ inline float fresnel(f4 n, f4 d, float ior) {
-  float k = cl_pow((ior - 1) / (ior + 1), 2.0f);
+  float k = cl_pow(cl_div(ior - 1, ior + 1), 2.0f);
   return k + (1 - k) * cl_pow(1 - __builtin_fabsf(cl_dot3(n.xyz, d.xyz)), 5.0f);
 }
 

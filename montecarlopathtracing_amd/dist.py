@@ -3,9 +3,12 @@
 Pixels are independent in the reference (per-pixel seed chain, history and
 count; read-only scene), so rank r renders the 16-row stripes s with
 s % world == r and no data moves during the frame loop.  At the end the
-zero-elsewhere accumulators are summed onto rank 0 by ONE reduce per buffer
-(RCCL over xGMI with the nccl backend; gloo on CPU in tests), giving exactly
-the single-GPU image for any GPU count.
+zero-elsewhere accumulators (mean, count, seed: 24 B per pixel) are packed
+into one flat int32 buffer and summed onto rank 0 by ONE reduce (RCCL over
+xGMI with the nccl backend; gloo on CPU in tests).  Each pixel has exactly
+one non-zero contributor, so the integer sum of bit patterns is that
+contributor's bits — exact for floats too, -0.0 included — giving the
+single-GPU image for any GPU count.
 """
 import numpy as np
 import torch
@@ -38,20 +41,24 @@ def ownership_mask(width, height, stripe_rows, rank, world):
 
 
 def reduce_image(hist, count, seeds, mask, group=None, dst=0):
-    """Sum every rank's owned pixels onto rank `dst`.
+    """Sum every rank's owned pixels onto rank `dst` with one collective.
 
     hist (N,4) float32, count (N,) int32, seeds (N,) int32 view of u32 — any
-    device the process group's backend supports.  Non-owned pixels are zeroed
-    before the reduce, so the sum is exact (one contributor per pixel)."""
+    device the process group's backend supports.  Non-owned pixels are zeroed,
+    the three arrays packed as int32 bit patterns into one (N, 6) buffer and
+    reduced with an integer SUM (one contributor per pixel: exact bits).
+    Returns (hist float32 (N,4), count int32, seeds int64 holding the u32)."""
     if hist.is_cuda and dist.get_backend(group) == "gloo":  # gloo reduces host tensors
         hist, count, seeds = hist.cpu(), count.cpu(), seeds.cpu()
     m = torch.as_tensor(mask, device=hist.device)
-    h = torch.where(m[:, None], hist, torch.zeros_like(hist))
-    c = torch.where(m, count, torch.zeros_like(count))
-    s = torch.where(m, seeds.to(torch.int64) & 0xFFFFFFFF, torch.zeros_like(seeds, dtype=torch.int64))
-    for t in (h, c, s):
-        dist.reduce(t, dst=dst, op=dist.ReduceOp.SUM, group=group)
-    return h, c, s  # seeds as int64 holding the u32 value
+    flat = torch.empty((hist.shape[0], 6), dtype=torch.int32, device=hist.device)
+    flat[:, :4] = hist.contiguous().view(torch.int32)
+    flat[:, 4] = count
+    flat[:, 5] = seeds.view(torch.int32) if seeds.dtype == torch.int32 else seeds.to(torch.int32)
+    flat.masked_fill_(~m[:, None], 0)
+    dist.reduce(flat, dst=dst, op=dist.ReduceOp.SUM, group=group)
+    h = flat[:, :4].contiguous().view(torch.float32)
+    return h, flat[:, 4].contiguous(), flat[:, 5].to(torch.int64) & 0xFFFFFFFF
 
 
 def render_distributed(renderer, scene, camera, width, height, max_depth, max_attempt, frames, seeds,

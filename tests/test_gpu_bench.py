@@ -38,12 +38,13 @@ def test_bench_two_ranks_rehearsal():
     lines = _lines(r.stdout)
     assert len(lines) == 1, r.stdout  # rank 0 only
     j = lines[0]
-    # headline: the fixed 1024x1024 image striped over the ranks (strong);
-    # the weak-scaled leg (a 1024x2048 image, 1024x1024 per rank) beside it
-    assert j["n_gpus"] == 2 and j["steps"] == 4 and j["scaling"] == "strong"
+    # headline: weak scaling, a 1024x2048 image, a 1024x1024 share per rank
+    # (the path partitions: no data-path collective); the strong-scaled leg
+    # (the fixed 1024x1024 image striped over the ranks) beside it
+    assert j["n_gpus"] == 2 and j["steps"] == 4 and j["scaling"] == "weak"
     assert j["value"] > 0 and j["config"]["parallelism"] == "row-stripe tiles x2"
-    assert j["config"]["width"] == 1024 and j["config"]["height"] == 1024
-    assert j["weak_scaling"]["value"] > 0 and j["weak_scaling"]["image"] == [1024, 2048]
+    assert j["config"]["width"] == 1024 and j["config"]["height"] == 2048
+    assert j["strong_scaling"]["value"] > 0 and j["strong_scaling"]["image"] == [1024, 1024]
     assert j["cpu_baseline"] is None  # rank 0 at N=1 only
     assert j["image_reduce_ms"] is not None and j["image_reduce_ms"] > 0  # the final image reduce ran
 
@@ -56,7 +57,7 @@ def test_bench_c4_strong_two_ranks_rehearsal():
                        capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stderr[-3000:]
     j = _lines(r.stdout)[0]
-    assert j["scaling"] == "strong" and j["config"]["height"] == 1080 and j["weak_scaling"] is None
+    assert j["scaling"] == "strong" and j["config"]["height"] == 1080 and j["strong_scaling"] is None
     assert j["image_reduce_ms"] is not None
 
 
@@ -73,7 +74,11 @@ def test_bench_default_line():
     assert j["n_gpus"] == 1 and j["steps"] == 8 and j["value"] > 0
     roof = j["roofline"]
     assert roof["bound"] == "hbm" and roof["peak"] == 8000.0
-    for k in ("frac", "issue_frac"):
+    for k in ("frac", "issue_frac", "valu_lane_utilization"):
         assert roof.get(k) is None or 0.0 <= roof[k] <= 1.0, (k, roof.get(k))
+    # the primary-hit cache serves each pixel's first segment of each frame
+    assert roof["segments_cache_served"] == 1024 * 1024 * 8
+    assert roof["segments_traced"] > 0
+    assert j["primary_cache_off"]["value"] > 0
     cpu = j["cpu_baseline"]
     assert cpu["cores"] >= 1 and cpu["threads"] == cpu["cores"] and cpu["cpu_model"] and cpu["value"] > 0

@@ -596,3 +596,30 @@ def test_render_zero_frames_and_bad_params(rnd):
     with pytest.raises(L.MCPTError):
         rnd.render_frames(dsc, cam, st, 4, 4, -1)
     dsc.close()
+
+
+def test_handoff_tag_wrap_bitexact(rnd):
+    """Block hand-off tags carry 8 bits of launch sequence: after 255 launches
+    they wrap and mcpt_render_frames clears the granule area first.  300 calls
+    of two one-frame blocks (one hand-off per pixel each) cross the wrap; the
+    image equals one 600-frame call's (255 blocks per launch: 3 launches) and
+    the reference kernels' bit for bit."""
+    data, cam = scenes.cbox(), S.parse_camera(scenes.CBOX_CAM)
+    w, h, depth = 24, 16, 4
+    seeds = R.default_seeds(w * h, variant="msvc15")
+    dsc = rnd.upload(data)
+    att = 1024  # a MAX_ATTEMPT the reference's history kernel is built for (oracle/Makefile)
+    a = rnd.new_state(w, h, seeds)
+    for _ in range(300):
+        rnd.render_frames(dsc, cam, a, depth, att, 2, frames_per_launch=1)
+        assert rnd.stats()["frames_per_block"] == 1
+    b = rnd.new_state(w, h, seeds)
+    rnd.render_frames(dsc, cam, b, depth, att, 600, frames_per_launch=1)
+    assert rnd.stats()["launches"] == 3
+    for x, y, what in ((a.hist, b.hist, "hist"), (a.count, b.count, "count"), (a.seeds, b.seeds, "seeds")):
+        assert_bits_equal(x.cpu().numpy(), y.cpu().numpy(), what)
+    if refgpu.available():
+        rh, rc, rs = refgpu.render(data, cam, w, h, depth, 600, att, seeds)
+        assert_bits_equal(b.hist.cpu().numpy(), rh, "hist vs reference")
+        assert_bits_equal(b.seeds_np(), rs, "seeds vs reference")
+    dsc.close()

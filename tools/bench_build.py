@@ -3,7 +3,9 @@ metric but reported): the reference HLBVH on the host (mcpt_build_hlbvh, the
 restated hlbvh.cpp) vs on the GPU (mcpt_build_hlbvh_device, same bits), and
 mcpt_scene_upload (device copies + the EXACT path's SAH search tree), and the
 treelet pass ("bvhtype": "treelet") on the GPU vs the CPU oracle's sequential
-restatement of TreeletBVH<CPU> (the reference's own algorithm, single thread).
+restatement of TreeletBVH<CPU> (the reference's own algorithm, single thread),
+and the GPU treelet kernel's pass every render runs (TreeletBVH<GPU>,
+mcpt_treelet_gpu_device) vs its sequential CPU restatement.
 
     python tools/bench_build.py [C2 C5 ...]  -> one JSON line per workload
 """
@@ -58,6 +60,26 @@ def main():
                 tl_same = bool(rc == 0 and np.array_equal(R.records(dn, L.BVHNODE).view(np.uint8), ref.view(np.uint8)))
         except ImportError:
             pass
+        dn = R.build_hlbvh_device(dt)
+        R.treelet_gpu_device(dn)  # warm
+        dn = R.build_hlbvh_device(dt)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        R.treelet_gpu_device(dn)
+        torch.cuda.synchronize()
+        t_tg = time.perf_counter() - t0
+        t_tg_cpu, tg_same = None, None
+        try:
+            from tests import oracle as O
+            from tests import refgpu
+            if O.available() and refgpu.available():
+                rcp = int(refgpu.rcp_f32(O.root_area_mant(host))[0].view(np.uint32))
+                t0 = time.perf_counter()
+                rc, ref, _ = O.treelet_gpu(host, rcp_bits=rcp)
+                t_tg_cpu = time.perf_counter() - t0
+                tg_same = bool(rc == 0 and np.array_equal(R.records(dn, L.BVHNODE).view(np.uint8), ref.view(np.uint8)))
+        except ImportError:
+            pass
         rnd = R.Renderer(0)
         t0 = time.perf_counter()
         sc = rnd.upload(data)
@@ -70,6 +92,9 @@ def main():
                           "scene_upload_s": round(t_up, 4), "treelet_gpu_s": round(t_tl, 4),
                           "treelet_cpu_oracle_s": None if t_tl_cpu is None else round(t_tl_cpu, 4),
                           "treelet_gpu_equals_oracle": tl_same,
+                          "treelet_gpu_kernel_pass_s": round(t_tg, 4),
+                          "treelet_gpu_kernel_pass_cpu_oracle_s": None if t_tg_cpu is None else round(t_tg_cpu, 4),
+                          "treelet_gpu_kernel_pass_equals_oracle": tg_same,
                           "note": "scene_upload = validation + 4-wide trees (reference collapse + SAH search "
                                   "tree, host, 16 threads) + device copies"}), flush=True)
 

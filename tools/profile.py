@@ -47,7 +47,7 @@ PASSES = {
     "derived": ["VALUBusy", "VALUUtilization"],
 }
 HBM_PEAK_GBS = 8000.0
-N_CU = 256
+N_CU_DEFAULT = 256  # MI355X; summarize() reads the profiled device's count (device.json)
 
 
 def sh(cmd, log, limit):
@@ -74,12 +74,16 @@ def run(tag, args):
     # the same command with the schedule the bench line's tuning picked, so
     # every pass profiles the same kernel instantiation
     cfg = json.loads(line.splitlines()[-1])["config"]
-    quiet = bench + ["--no-cpu", "--schedule", cfg["schedule"], "--shade-threshold", str(cfg.get("shade_threshold", 32)),
+    quiet = bench + ["--no-cpu", "--no-cache-off", "--schedule", cfg["schedule"], "--shade-threshold", str(cfg.get("shade_threshold", 32)),
                      "--fetch-threshold", str(cfg.get("fetch_threshold", 1)),
                      "--block-entries", str(cfg.get("block_entries", 32))]
     sh(["rocprofv3", "--kernel-trace", "--stats", "--output-format", "csv", "-d", os.path.join(out, "trace"), "--"]
        + quiet, os.path.join(out, "trace.log"), 400)
     print("trace done", flush=True)
+    # the CU count the busy ratios divide by, read from the device
+    sh([sys.executable, "-c", "import json, torch; p = torch.cuda.get_device_properties(0); "
+        "json.dump({'cus': p.multi_processor_count, 'name': p.name}, open(%r, 'w'))" % os.path.join(out, "device.json")],
+       os.path.join(out, "device.log"), 120)
     for name, ctrs in PASSES.items():
         sh(["rocprofv3", "--pmc"] + ctrs + ["--output-format", "csv", "-d", os.path.join(out, "pmc_" + name), "--"]
            + quiet, os.path.join(out, "pmc_%s.log" % name), 300)
@@ -166,6 +170,10 @@ def summarize(tag):
     wr = ctr["WRITE_SIZE"] * 1024.0
     rd = rd_raw * fetch_scale
     secs = timed_ms / 1e3
+    try:
+        N_CU = int(json.load(open(os.path.join(src, "device.json")))["cus"])
+    except (OSError, ValueError, KeyError):
+        N_CU = N_CU_DEFAULT
     grbm = ctr["GRBM_GUI_ACTIVE"]  # summed over the 8 XCDs (MI355X_MICROARCH.md)
     cycles = grbm / 8.0
     l2_req = ctr["TCC_HIT_sum"] + ctr["TCC_MISS_sum"]
@@ -187,7 +195,7 @@ def summarize(tag):
                         "scale_128": round(s128, 4), "scale_64": round(s64, 4), "weight_128": round(w128, 4)},
         "hbm_read_bytes": rd, "hbm_write_bytes": wr, "hbm_bytes": rd + wr,
         "hbm_GBps": round((rd + wr) / secs / 1e9, 2), "hbm_frac": round((rd + wr) / secs / 1e9 / HBM_PEAK_GBS, 5),
-        "kernel_cycles": cycles, "clock_GHz": round(cycles / secs / 1e9, 3),
+        "kernel_cycles": cycles, "clock_GHz": round(cycles / secs / 1e9, 3), "cus": N_CU,
         "valu_busy": round(ctr["SQ_ACTIVE_INST_VALU"] / (N_CU * cycles), 4),
         "valu_busy_rocprof_derived": round(ctr.get("VALUBusy", float("nan")) / 100.0, 4),
         "valu_utilization_lanes": round(ctr.get("VALUUtilization", float("nan")) / 100.0, 4),
@@ -211,14 +219,17 @@ def summarize(tag):
             "traffic": rd + wr, "avg_launch_ms": r.get("avg_launch_ms"),
             "achieved": round((rd + wr) / (r["avg_launch_ms"] / 1e3) / 1e9, 2) if r.get("avg_launch_ms") else None,
             "frac": round((rd + wr) / (r["avg_launch_ms"] / 1e3) / 1e9 / HBM_PEAK_GBS, 5) if r.get("avg_launch_ms") else None,
-            "issue_frac": round(ctr["SQ_ACTIVE_INST_VALU"] / (N_CU * cycles), 4),
+            "valu_busy": round(ctr["SQ_ACTIVE_INST_VALU"] / (N_CU * cycles), 4),
+            "issue_frac": round(ctr["SQ_ACTIVE_INST_VALU"] / (N_CU * cycles) * ctr.get("VALUUtilization", float("nan")) / 100.0, 4),
             "td_busy": round(ctr.get("TD_TD_BUSY_sum", float("nan")) / (N_CU * cycles), 4)},
         "counters_timed_dispatch": ctr,
         "sources": ["profiles/%s_%s.csv" % (tag, x) for x in
                     ["kernel_stats", "kernel_trace"] + ["pmc_" + n for n in PASSES] + ["calib_fetch", "calib_write"]],
         "note": "counters of the timed launch only (last dispatch of the bench's non-counting k_render); "
                 "GRBM_GUI_ACTIVE is summed over the 8 XCDs (cycles = /8); SQ_* cycle counters are quad-cycles; "
-                "valu_busy = SQ_ACTIVE_INST_VALU / (CUs x cycles) (rocprofv3's VALUBusy definition); "
+                "valu_busy = SQ_ACTIVE_INST_VALU / (CUs x cycles) (rocprofv3's VALUBusy definition; it can read ~1 % "
+                "over 1 on a VALU-saturated kernel, as rocprofv3's own VALUBusy does); issue_frac = valu_busy x "
+                "VALUUtilization (lane-weighted); "
                 "hbm bytes = FETCH_SIZE x calibrated scale + WRITE_SIZE (memory-side: Infinity-Cache hits included)",
     }
     with open(os.path.join(dst, tag + "_summary.json"), "w") as fh:
@@ -232,6 +243,7 @@ def summarize(tag):
     allw = {k: v for k, v in allw.items() if "@" in k}  # drop the round-1 layout
     allw[key] = {"hbm_bytes_per_launch": rd + wr, "hbm_read_bytes_per_launch": rd, "hbm_write_bytes_per_launch": wr,
                  "fetch_scale_calibrated": summ["fetch_scale_calibrated"], "valu_busy": summ["valu_busy"],
+                 "valu_utilization_lanes": summ["valu_utilization_lanes"],
                  "ta_busy": summ["ta_busy"], "td_busy": summ["td_busy"],
                  "wave_wait_any_per_wave_cycle": summ["wave_wait_any_per_wave_cycle"],
                  "l2_hit_rate": summ["l2_hit_rate"], "l1_hit_rate": summ["l1_hit_rate"],
