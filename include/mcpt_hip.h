@@ -274,6 +274,20 @@ int mcpt_scene_upload(mcpt_ctx *ctx, const mcpt_triangle *tris, int64_t n_tris,
                       const mcpt_bvh_node *nodes, int64_t n_nodes,
                       const mcpt_material *mats, int32_t n_mats, mcpt_scene **out);
 int mcpt_scene_destroy(mcpt_scene *scene);
+/* The same with the scene already in HBM (tris_dev packed as
+ * mcpt_pack_triangles leaves them, nodes_dev in the HLBVH layout, e.g. from
+ * mcpt_build_hlbvh_device + mcpt_treelet_gpu_device): every device structure,
+ * the EXACT path's SAH search tree included, built on the GPU, the same
+ * bytes as mcpt_scene_upload's.  Synchronises `stream`.                  */
+int mcpt_scene_upload_device(mcpt_ctx *ctx, const mcpt_triangle *tris_dev, int64_t n_tris,
+                             const mcpt_bvh_node *nodes_dev, int64_t n_nodes, const mcpt_material *mats,
+                             int32_t n_mats, void *stream, mcpt_scene **out);
+/* A scene's device arrays copied to the host (introspection).  which: 0 the
+ * search tree (128-B nodes), 1 its quantized nodes, 2 the reference tree
+ * 4-wide, 3 the binary child-box nodes, 4 triangles, 5 quantized-path
+ * triangles, 6 int32[4] {stack_depth, stack_depth4, quantized, n_internal}.
+ * *bytes = the size (host NULL: size only).                               */
+int mcpt_scene_read(const mcpt_scene *scene, int32_t which, void *host, int64_t cap, int64_t *bytes);
 
 /* Fused per-pixel path loop: for every pixel of this GPU's stripes and
  * frames [frame_begin, frame_begin+frames): generateRay -> maxdepth x

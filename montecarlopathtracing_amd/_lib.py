@@ -88,6 +88,8 @@ SIGNATURES = {
     "mcpt_device_count": (_I32, [_P]),
     "mcpt_scene_upload": (_I32, [_P, _P, _I64, _P, _I64, _P, _I32, _P]),
     "mcpt_scene_destroy": (_I32, [_P]),
+    "mcpt_scene_upload_device": (_I32, [_P, _P, _I64, _P, _I64, _P, _I32, _P, _P]),
+    "mcpt_scene_read": (_I32, [_P, _I32, _P, _I64, _P]),
     "mcpt_render_frames": (_I32, [_P, _P, _P, _P, _P, _P, _P, _P]),
     "mcpt_generate_rays": (_I32, [_P, _P, _I32, _I32, _P, _P]),
     "mcpt_intersect": (_I32, [_P, _P, _P, _I64, _P, _F32, _I32, _P]),

@@ -33,6 +33,7 @@
 #include "../../include/mcpt_hip.h"
 #include "mcpt_refmath.h"
 #include "mcpt_bvh4.h"
+#include "mcpt_upload.h"
 
 using namespace mcpt;
 
@@ -140,6 +141,7 @@ struct mcpt_scene {
   int64_t n_tris = 0, n_internal = 0;
   int32_t n_mats = 0;
   int32_t stack_depth = 1;
+  bool has_glossy = true;  // any GLOSSY material: k_render's glossy-lobe shading path
   SceneView view;
 };
 
@@ -570,25 +572,40 @@ struct ShadeOut {
 // fused kernel leaves such a lane in its S phase, where its next draw shares
 // the one randomDirection call site with every other lane's first draw
 // (diffuse, and glossy either lobe), instead of holding the whole wave in
-// the loop.
+// the loop.  G = false: a scene without glossy materials (C2's diffuse-only
+// override, C5): the diffuse lobe alone, no coin, never pending.
+template <bool G = true>
 __device__ inline ShadeOut shade_hit(const mcpt_material *__restrict__ mats, const ShadeIn &in, f4 color,
                                      uint32_t &seed, int max_depth, bool &resample) {
   ShadeOut r;
   r.bad = false;
   r.new_ray = true;
   r.pending = false;
-  const mcpt_material M = mats[in.mat];
-  const f4 kd = (f4){M.kd[0], M.kd[1], M.kd[2], M.kd[3]};
-  const f4 kaks = (f4){M.ka_ks[0], M.ka_ks[1], M.ka_ks[2], M.ka_ks[3]};
+  // material fields are read where they are used (the table is in LDS): the
+  // draw below keeps fewer values live
+  const mcpt_material *__restrict__ Mp = mats + in.mat;
+  const int32_t type = Mp->type;
+  auto kd_of = [&]() { return (f4){Mp->kd[0], Mp->kd[1], Mp->kd[2], Mp->kd[3]}; };
+  auto kaks_of = [&]() { return (f4){Mp->ka_ks[0], Mp->ka_ks[1], Mp->ka_ks[2], Mp->ka_ks[3]}; };
   int32_t td = as_i(in.o.w);
   f4 no, nd;
-  switch (M.type) {
+  if (!G && type == MCPT_GLOSSY) goto bad_material;  // excluded by the G = false scene check
+  switch (type) {
     case MCPT_DIFFUSE:
     case MCPT_GLOSSY: {
+      if constexpr (!G) {
+        nd = random_dir(in.nrm, seed);
+        no = in.pt + kEps * nd;
+        no.w = as_f(td + 1);
+        nd.w = in.d.w;
+        color = cl_div4(color * kd_of() * cl_dot3(nd.xyz, in.nrm.xyz), (float)(2 * kClPi));
+        break;
+      }
       // glossy: the lobe coin (shade.cl:115), then the Phong lobe around the
       // mirror direction, else the diffuse lobe (shade.cl:139)
-      const bool lobe = resample || (M.type == MCPT_GLOSSY && (lcg15(seed) & 0x00000001));
-      const f4 axis = lobe ? mirror_dir(in.nrm, in.d) : in.nrm;
+      const bool lobe = resample || (type == MCPT_GLOSSY && (lcg15(seed) & 0x00000001));
+      f4 axis = in.nrm;
+      if (lobe) axis = mirror_dir(in.nrm, in.d);
       nd = random_dir(axis, seed);
       if (lobe && cl_dot3(nd.xyz, in.nrm.xyz) <= 0) {  // rejected: draw again next call
         resample = true;
@@ -600,8 +617,12 @@ __device__ inline ShadeOut shade_hit(const mcpt_material *__restrict__ mats, con
       no.w = as_f(td + 1);
       nd.w = in.d.w;
       // diffuse: color * kd * cos / 2pi; glossy: color * ks * pow(cos_r, Ns) * cos / 2pi
-      f4 c = color * (lobe ? kaks : kd);
-      if (lobe) c = c * cl_pow(cl_dot3(nd.xyz, axis.xyz), M.Ns);
+      // (the mirror direction recomputed rather than kept live across the draw)
+      f4 c;
+      if (lobe)
+        c = color * kaks_of() * cl_pow(cl_dot3(nd.xyz, mirror_dir(in.nrm, in.d).xyz), Mp->Ns);
+      else
+        c = color * kd_of();
       color = cl_div4(c * cl_dot3(nd.xyz, in.nrm.xyz), (float)(2 * kClPi));
       break;
     }
@@ -610,12 +631,13 @@ __device__ inline ShadeOut shade_hit(const mcpt_material *__restrict__ mats, con
       r.o = in.o;
       r.o.w = as_f(td | (int32_t)MCPT_TERMINATED);
       r.d = in.d;
-      r.color = color * kaks;
+      r.color = color * kaks_of();
       return r;
     case MCPT_TRANSPARENT: {
+      const float Ni = Mp->Ni;
       bool inside = (td & 0x00FF0000) != 0;
-      float ei = inside ? M.Ni : 1.0f;
-      float et = inside ? 1.0f : M.Ni;
+      float ei = inside ? Ni : 1.0f;
+      float et = inside ? 1.0f : Ni;
       if (!transmit_dir(in.nrm, in.d, ei, et, nd)) {  // total internal reflection
         no = in.pt;
         nd = mirror_dir(in.nrm, in.d);
@@ -623,11 +645,11 @@ __device__ inline ShadeOut shade_hit(const mcpt_material *__restrict__ mats, con
         no.w = as_f(td + 1);
         break;
       }
-      float fr = fresnel(in.nrm, nd, M.Ni);
+      float fr = fresnel(in.nrm, nd, Ni);
       no = in.pt;
       nd.w = in.d.w;
       int32_t ntd = td + 1;
-      if (cl_div(lcg15(seed) * 1.0f, 32768) >= fr) {
+      if (lcg15(seed) * 1.0f * 0x1p-15f >= fr) {  // x / 32768, exact either way
         ntd ^= 0x00FF0000;
       } else {
         nd.xyz = mirror_dir(in.nrm, in.d).xyz;
@@ -636,6 +658,7 @@ __device__ inline ShadeOut shade_hit(const mcpt_material *__restrict__ mats, con
       break;
     }
     default:  // the reference leaves newRay uninitialised here; we end the path
+    bad_material:
       r.bad = true;
       r.new_ray = false;
       r.o = in.o;
@@ -776,7 +799,7 @@ __device__ inline uint32_t queue_items(uint32_t x, uint32_t n_tiles, uint32_t nq
 // PRIM: the primary-hit pass (PrimHit) run by the same machine: one frame,
 // no pixel state; a lane traces its pixel's primary ray, stores the closest
 // hit at the S phase instead of shading, and takes the next pixel.
-template <int MODE, bool STATS, bool WIN, bool PAIR, bool Q, bool PRIM = false>
+template <int MODE, bool STATS, bool WIN, bool PAIR, bool Q, bool PRIM = false, bool G = true>
 __global__ void __launch_bounds__(64, MCPT_WAVES_PER_SIMD) k_render(RenderArgs A) {
   constexpr bool PRUNE = MODE != MCPT_MODE_NOPRUNE;
   constexpr bool LIT = MODE == MCPT_MODE_NOPRUNE;
@@ -900,7 +923,7 @@ __global__ void __launch_bounds__(64, MCPT_WAVES_PER_SIMD) k_render(RenderArgs A
       // lanes that need an entry start together once th_fetch of them wait
       // (their state loads then share one wait), or when no lane is busy
       const unsigned long long mn = __ballot(lst == kNeed);
-      if (mn && (__popcll(mn) >= A.th_fetch || !__ballot(lst <= kBusy))) {
+      if (mn && (__popcll(mn) >= A.th_fetch || !__ballot(G ? lst <= kBusy : lst == kBusy))) {
         const uint32_t n_need = (uint32_t)__popcll(mn);
         const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(mn >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mn, 0));
         uint32_t q = pool + rank, qx = (qs >> 4) & 15u;
@@ -986,7 +1009,7 @@ __global__ void __launch_bounds__(64, MCPT_WAVES_PER_SIMD) k_render(RenderArgs A
     }
     MCPT_TICK(0);
     if (!__ballot(lst != kDead)) break;
-    const bool live = lst <= kBusy;
+    const bool live = G ? lst <= kBusy : lst == kBusy;  // (kRes only with glossy materials)
     // phase thresholds scaled to the wave's live lanes: a wave with few pixels
     // (a launch's tail, a strong-scaled rank) does not wait for lane counts
     // only a full wave reaches (C2 -3 %, C5 -4 %, C2 4- and 8-rank shares
@@ -1175,8 +1198,8 @@ __global__ void __launch_bounds__(64, MCPT_WAVES_PER_SIMD) k_render(RenderArgs A
           if (cl_dot3(d.xyz, in.nrm.xyz) > 0) in.nrm = -in.nrm;  // intersect.cl:23-25
           in.pt = o + best_t * d;                                  // objdef.h:218
           in.mat = as_i(tn.w);
-          bool rs = lst == kRes;
-          ShadeOut so = shade_hit(mats, in, color, seed, A.max_depth, rs);
+          bool rs = G && lst == kRes;
+          ShadeOut so = shade_hit<G>(mats, in, color, seed, A.max_depth, rs);
           pending = so.pending;
           lst = pending ? kRes : kBusy;
           if (!pending) {
@@ -1896,6 +1919,8 @@ int mcpt_scene_upload(mcpt_ctx *ctx, const mcpt_triangle *tris, int64_t n_tris, 
   s->near4_bytes = (int64_t)(near.size() * sizeof(DevNode4));
   s->n_internal = n_int;
   s->n_mats = n_mats;
+  s->has_glossy = false;
+  for (int32_t k = 0; k < n_mats; ++k) s->has_glossy |= mats[k].type == MCPT_GLOSSY;
   s->stack_depth = std::max(depth, 1);
   s->stack_depth4 = depth4;
   SceneView &v = s->view;
@@ -1916,6 +1941,104 @@ int mcpt_scene_upload(mcpt_ctx *ctx, const mcpt_triangle *tris, int64_t n_tris, 
   v.n_mats = n_mats;
   v.prune_margin = std::isfinite(diag) ? std::ldexp(diag, -10) : __builtin_inff();
   *out = s;
+  return MCPT_OK;
+}
+
+// SceneBuild::buildScene with the scene already in HBM: every device
+// structure of mcpt_scene_upload, built on the GPU (mcpt_upload.hip), the
+// same bytes.
+int mcpt_scene_upload_device(mcpt_ctx *ctx, const mcpt_triangle *tris_dev, int64_t n_tris,
+                             const mcpt_bvh_node *nodes_dev, int64_t n_nodes, const mcpt_material *mats,
+                             int32_t n_mats, void *stream, mcpt_scene **out) {
+  if (!ctx || !tris_dev || !nodes_dev || !mats || !out || n_tris <= 0 || n_mats <= 0)
+    return mcpt::fail(MCPT_ERR_ARG, "scene_upload_device: bad argument");
+  if (n_nodes != 2 * n_tris - 1) return mcpt::fail(MCPT_ERR_ARG, "scene_upload_device: expected 2n-1 BVH nodes");
+  HIP_OK(hipSetDevice(ctx->device));
+  mcpt::DeviceScene D;
+  int rc = mcpt::build_scene_device(tris_dev, n_tris, nodes_dev, n_mats, (hipStream_t)stream, &D);
+  auto free_d = [&]() {
+    for (void *p : {D.near4, D.near4q, D.nodes4, D.nodes, D.tris, D.triq})
+      if (p) (void)hipFree(p);
+  };
+  if (rc != MCPT_OK) {
+    free_d();
+    return rc;
+  }
+  static std::atomic<uint64_t> scene_uids_d{1ull << 62};  // distinct from mcpt_scene_upload's
+  mcpt_scene *s = new mcpt_scene();
+  s->uid = ++scene_uids_d;
+  s->device = ctx->device;
+  s->near4 = (DevNode4 *)D.near4;
+  s->near4q = (DevNode4Q *)D.near4q;
+  s->nodes4 = (DevNode4 *)D.nodes4;
+  s->nodes = (DevNode *)D.nodes;
+  s->tris = (DevTri *)D.tris;
+  s->triq = (DevTriQ *)D.triq;
+  if (hipMalloc(&s->mats, n_mats * sizeof(mcpt_material)) != hipSuccess ||
+      hipMemcpy(s->mats, mats, n_mats * sizeof(mcpt_material), hipMemcpyHostToDevice) != hipSuccess) {
+    mcpt_scene_destroy(s);
+    return mcpt::fail(MCPT_ERR_HIP, "scene_upload_device: material upload failed");
+  }
+  const mcpt_bvh_node &root = D.root;
+  s->n_tris = n_tris;
+  s->near4_bytes = D.n_near4 * (int64_t)sizeof(DevNode4);
+  s->n_internal = D.n_int;
+  s->n_mats = n_mats;
+  s->has_glossy = false;
+  for (int32_t k = 0; k < n_mats; ++k) s->has_glossy |= mats[k].type == MCPT_GLOSSY;
+  s->stack_depth = std::max(D.stack_depth, 1);
+  s->stack_depth4 = D.depth4;
+  float dx = root.bbmax[0] - root.bbmin[0], dy = root.bbmax[1] - root.bbmin[1], dz = root.bbmax[2] - root.bbmin[2];
+  float diag = std::sqrt(dx * dx + dy * dy + dz * dz);
+  SceneView &v = s->view;
+  v.n_near4 = (int32_t)D.n_near4;
+  v.n_nodes4 = (int32_t)D.n_nodes4;
+  v.n_int = (int32_t)std::max<int64_t>(D.n_int, 1);
+  v.n_tris = n_tris;
+  v.nodes = s->nodes;
+  v.nodes4 = s->nodes4;
+  v.near4 = s->near4;
+  v.tris = s->tris;
+  v.near4q = s->near4q;
+  v.triq = s->triq;
+  v.mats = s->mats;
+  v.root_min = (f4){root.bbmin[0], root.bbmin[1], root.bbmin[2], root.bbmin[3]};
+  v.root_max = (f4){root.bbmax[0], root.bbmax[1], root.bbmax[2], root.bbmax[3]};
+  v.root_leaf = root.left == root.right ? root.left : -1;
+  v.n_mats = n_mats;
+  v.prune_margin = std::isfinite(diag) ? std::ldexp(diag, -10) : __builtin_inff();
+  *out = s;
+  return MCPT_OK;
+}
+
+// A scene's device arrays, copied to the host (introspection: tests compare
+// the two upload paths byte for byte).  which: 0 near4, 1 near4q, 2 nodes4,
+// 3 nodes, 4 tris, 5 triq, 6 int32[4] {stack_depth, stack_depth4, quantized,
+// n_internal}.  *bytes = the array's size; host may be NULL to ask for it.
+int mcpt_scene_read(const mcpt_scene *s, int32_t which, void *host, int64_t cap, int64_t *bytes) {
+  if (!s || !bytes) return mcpt::fail(MCPT_ERR_ARG, "scene_read: bad argument");
+  const void *src = nullptr;
+  int64_t n = 0;
+  int32_t meta[4] = {s->stack_depth, s->stack_depth4, s->near4q ? 1 : 0, (int32_t)s->n_internal};
+  switch (which) {
+    case 0: src = s->near4, n = (int64_t)s->view.n_near4 * (int64_t)sizeof(DevNode4); break;
+    case 1: src = s->near4q, n = s->near4q ? (int64_t)s->view.n_near4 * (int64_t)sizeof(DevNode4Q) : 0; break;
+    case 2: src = s->nodes4, n = (int64_t)s->view.n_nodes4 * (int64_t)sizeof(DevNode4); break;
+    case 3: src = s->nodes, n = (int64_t)s->view.n_int * (int64_t)sizeof(DevNode); break;
+    case 4: src = s->tris, n = s->n_tris * (int64_t)sizeof(DevTri); break;
+    case 5: src = s->triq, n = s->triq ? s->n_tris * (int64_t)sizeof(DevTriQ) : 0; break;
+    case 6: n = sizeof(meta); break;
+    default: return mcpt::fail(MCPT_ERR_ARG, "scene_read: unknown array");
+  }
+  *bytes = n;
+  if (!host) return MCPT_OK;
+  if (cap < n) return mcpt::fail(MCPT_ERR_ARG, "scene_read: buffer too small");
+  if (which == 6) {
+    std::memcpy(host, meta, sizeof(meta));
+    return MCPT_OK;
+  }
+  HIP_OK(hipSetDevice(s->device));
+  if (n) HIP_OK(hipMemcpy(host, src, (size_t)n, hipMemcpyDeviceToHost));
   return MCPT_OK;
 }
 
@@ -2006,19 +2129,24 @@ int mcpt_render_frames(mcpt_ctx *ctx, const mcpt_scene *scene, const mcpt_camera
   // workgroups than a kStackWindow window does, the windowed kernel runs.
   const bool noprune = p->mode == MCPT_MODE_NOPRUNE;
   // [kind: 0 EXACT 128-B nodes, 1 NOPRUNE, 2 EXACT quantized][stats][window][pair]
-#define MCPT_KR(M, ST, W, QN) {(const void *)k_render<M, ST, W, false, QN>, (const void *)k_render<M, ST, W, true, QN>}
+  // [kind][stats][window][pair][glossy materials]
+#define MCPT_KG(M, ST, W, P, QN) {(const void *)k_render<M, ST, W, P, QN, false, false>, \
+                                  (const void *)k_render<M, ST, W, P, QN, false, true>}
+#define MCPT_KR(M, ST, W, QN) {MCPT_KG(M, ST, W, false, QN), MCPT_KG(M, ST, W, true, QN)}
 #define MCPT_KK(M, QN) {{MCPT_KR(M, false, false, QN), MCPT_KR(M, false, true, QN)}, \
                         {MCPT_KR(M, true, false, QN), MCPT_KR(M, true, true, QN)}}
-  static const void *const kfns[3][2][2][2] = {MCPT_KK(MCPT_MODE_EXACT, false), MCPT_KK(MCPT_MODE_NOPRUNE, false),
-                                               MCPT_KK(MCPT_MODE_EXACT, true)};
+  static const void *const kfns[3][2][2][2][2] = {MCPT_KK(MCPT_MODE_EXACT, false), MCPT_KK(MCPT_MODE_NOPRUNE, false),
+                                                  MCPT_KK(MCPT_MODE_EXACT, true)};
   // the primary-hit pass: [kind][window][pair], no stats
-#define MCPT_KP(M, W, QN) {(const void *)k_render<M, false, W, false, QN, true>, (const void *)k_render<M, false, W, true, QN, true>}
+#define MCPT_KP(M, W, QN) {(const void *)k_render<M, false, W, false, QN, true, false>, \
+                           (const void *)k_render<M, false, W, true, QN, true, false>}
   static const void *const kpfns[3][2][2] = {{MCPT_KP(MCPT_MODE_EXACT, false, false), MCPT_KP(MCPT_MODE_EXACT, true, false)},
                                              {MCPT_KP(MCPT_MODE_NOPRUNE, false, false), MCPT_KP(MCPT_MODE_NOPRUNE, true, false)},
                                              {MCPT_KP(MCPT_MODE_EXACT, false, true), MCPT_KP(MCPT_MODE_EXACT, true, true)}};
 #undef MCPT_KP
 #undef MCPT_KK
 #undef MCPT_KR
+#undef MCPT_KG
   // quantized search tree: forced on (1) or off (2), or auto (0): on when the
   // 128-B tree outgrows the GPU's aggregate L2, where its halved node bytes and
   // gathers pay (C5 -6 %); on cache-resident trees its looser boxes cost more
@@ -2026,6 +2154,7 @@ int mcpt_render_frames(mcpt_ctx *ctx, const mcpt_scene *scene, const mcpt_camera
   // profiles/r02_quant_ab.txt)
   const bool quant = scene->near4q && (T.quantized == 1 || (T.quantized == 0 && scene->near4_bytes > kQuantAutoBytes));
   const int kind = noprune ? 1 : (quant ? 2 : 0);
+  const int glossy = scene->has_glossy ? 1 : 0;  // the shading instantiation (speed only: same bits)
   const size_t pad = (size_t)std::max(0, T.lds_pad);
   const size_t lds_plain = (size_t)depth_entries * 64 * sizeof(int32_t) + sizeof(LdsUniforms) + lds_mats + pad;
   const size_t lds_win = (size_t)kStackWindow * 64 * sizeof(int32_t) + sizeof(LdsUniforms) + lds_mats + pad;
@@ -2033,22 +2162,22 @@ int mcpt_render_frames(mcpt_ctx *ctx, const mcpt_scene *scene, const mcpt_camera
   int per_cu = 0;
   if (T.stack_window == 1) {  // forced (tests, experiments): the window even when the whole stack fits in it
     win = true;
-    rc = occupancy(ctx, kfns[kind][ctx->stats_on][1][pair], lds_win, &per_cu);
+    rc = occupancy(ctx, kfns[kind][ctx->stats_on][1][pair][glossy], lds_win, &per_cu);
     if (rc) return rc;
   } else if (depth_entries > kStackWindow && T.stack_window != 2) {
     int per_cu_plain = 0, per_cu_win = 0;
-    rc = occupancy(ctx, kfns[kind][ctx->stats_on][0][pair], lds_plain, &per_cu_plain);
+    rc = occupancy(ctx, kfns[kind][ctx->stats_on][0][pair][glossy], lds_plain, &per_cu_plain);
     if (rc) return rc;
-    rc = occupancy(ctx, kfns[kind][ctx->stats_on][1][pair], lds_win, &per_cu_win);
+    rc = occupancy(ctx, kfns[kind][ctx->stats_on][1][pair][glossy], lds_win, &per_cu_win);
     if (rc) return rc;
     win = T.stack_window == 1 || per_cu_win > per_cu_plain;
     per_cu = win ? per_cu_win : per_cu_plain;
   } else {
-    rc = occupancy(ctx, kfns[kind][ctx->stats_on][0][pair], lds_plain, &per_cu);
+    rc = occupancy(ctx, kfns[kind][ctx->stats_on][0][pair][glossy], lds_plain, &per_cu);
     if (rc) return rc;
   }
   const size_t lds = win ? lds_win : lds_plain;
-  const void *kfn = kfns[kind][ctx->stats_on][win][pair];
+  const void *kfn = kfns[kind][ctx->stats_on][win][pair][glossy];
   A.stack_depth = win ? kStackWindow : depth_entries;  // the uniforms and material table follow the stack in LDS
   A.spill_stride = win ? std::max(0, depth_entries - kStackWindow) : 0;
   const int64_t grid = std::max<int64_t>(1, std::min<int64_t>(tiles, (int64_t)std::max(per_cu, 1) * ctx->n_cu));

@@ -174,7 +174,7 @@ __device__ inline float random_phi(uint32_t r) { return (float)(2 * kClPi / 3276
 __device__ inline f4 random_dir(f4 n, uint32_t &seed) {
   n.w = 0;
   float phi = random_phi(lcg15(seed));
-  float u = cl_div(lcg15(seed) * 1.0f, 32768);
+  float u = lcg15(seed) * 1.0f * 0x1p-15f;  // = the 2.5-ulp x / 32768: both exact for x < 2^24
   float s = cl_sqrt(u);
   float sin_phi, cos_phi;
   sincos_small(phi, sin_phi, cos_phi);

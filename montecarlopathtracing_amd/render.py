@@ -40,18 +40,40 @@ def default_seeds(n, variant="splitmix"):
 
 
 class DeviceScene:
-    """SceneBuild::buildScene result living in HBM (child-box node layout)."""
+    """SceneBuild::buildScene result living in HBM (child-box node layout).
+    `data` is a host SceneData (mcpt_scene_upload), or a tuple (tris, nodes,
+    mats) whose tris / nodes are device byte tensors (mcpt_scene_upload_device:
+    everything built on the GPU, the same bytes)."""
+
+    ARRAYS = ("near4", "near4q", "nodes4", "nodes", "tris", "triq")
 
     def __init__(self, renderer, data):
         self.renderer = renderer
         self.data = data
         self.handle = ctypes.c_void_p()
         self.schedule = L.SCHED_PAIRED  # k_render leaf-test schedule: paired measured faster on C2-C5 (tune_schedule)
+        if isinstance(data, tuple):
+            t, nd, mats = data
+            m = np.ascontiguousarray(mats)
+            n = t.numel() // L.TRIANGLE.itemsize
+            L.check(L.lib().mcpt_scene_upload_device(renderer.ctx, L.ptr(t), n, L.ptr(nd), nd.numel() // L.BVHNODE.itemsize,
+                                                     L.ptr(m), len(m), _stream(), ctypes.byref(self.handle)))
+            return
         t = np.ascontiguousarray(data.tris)
         nd = np.ascontiguousarray(data.nodes)
         m = np.ascontiguousarray(data.mats)
         L.check(L.lib().mcpt_scene_upload(renderer.ctx, L.ptr(t), len(t), L.ptr(nd), len(nd), L.ptr(m), len(m),
                                           ctypes.byref(self.handle)))
+
+    def read(self, which):
+        """One device array as bytes (mcpt_scene_read; which: a name of ARRAYS
+        or "meta" -> int32 {stack_depth, stack_depth4, quantized, n_internal})."""
+        k = 6 if which == "meta" else self.ARRAYS.index(which)
+        n = ctypes.c_int64()
+        L.check(L.lib().mcpt_scene_read(self.handle, k, None, 0, ctypes.byref(n)))
+        buf = np.zeros(n.value, np.uint8)
+        L.check(L.lib().mcpt_scene_read(self.handle, k, L.ptr(buf), n.value, ctypes.byref(n)))
+        return buf.view(np.int32) if which == "meta" else buf
 
     def close(self):
         if self.handle:

@@ -286,3 +286,67 @@ def test_gpu_lcv_equals_reference_host():
     w, h = (int(x) for x in g["lcv_size"])
     v = B.lcv(scenes.cbox().nodes, S.parse_camera(scenes.CBOX_CAM), w, h)
     assert np.float32(v).view(np.uint32) == g["lcv_cbox_bits"]
+
+
+# ------------------------------------ the scene's structures built on the GPU
+UPLOAD_CASES = ["cbox", "mis", "dining", "two", "three", "dup", "flat", "signed_zero", "rand5", "rand64", "rand1000",
+                "random200k"]
+
+
+class _Scene:  # what DeviceScene reads of a SceneData
+    def __init__(self, tris, nodes, mats):
+        self.tris, self.nodes, self.mats = tris, nodes, mats
+
+
+def _upload_both(tris, nodes, mats):
+    rnd = R.Renderer(0)
+    host = rnd.upload(_Scene(tris, nodes, mats))
+    dev = rnd.upload((R.to_device(tris, 0), R.to_device(nodes, 0), mats))
+    return rnd, host, dev
+
+
+@pytest.mark.parametrize("name", UPLOAD_CASES)
+def test_scene_upload_device_equals_host(name):
+    """mcpt_scene_upload_device (csrc/mcpt_upload.hip: validation, stack
+    bounds, the reference tree 4-wide, the binned-SAH search tree with its
+    4-wide collapse and emission order, the quantized nodes, the triangle
+    records, all on the GPU) == mcpt_scene_upload (host, mcpt_sah.cpp): every
+    device array byte for byte."""
+    named = {"cbox": scenes.cbox, "mis": scenes.mis, "dining": scenes.dining}
+    if name in named:
+        d = named[name]()
+        tris, mats = d.tris, d.mats
+    else:
+        tris, mats = _case(name), scenes.cbox().mats
+    nodes = R.treelet_gpu_device(S.build_hlbvh(tris))
+    rnd, host, dev = _upload_both(tris, nodes, mats)
+    for k in R.DeviceScene.ARRAYS + ("meta",):
+        a, b = host.read(k), dev.read(k)
+        assert a.tobytes() == b.tobytes(), (name, k, len(a), len(b))
+    host.close()
+    dev.close()
+    rnd.close()
+
+
+def test_scene_upload_device_c5_size_renders_bitexact():
+    """A 2M-triangle random mesh (C5's kind, large ranges split level by level
+    on the GPU): the device-built scene equals the host-built one array for
+    array, and renders the same bits."""
+    tris = S.random_mesh(2_000_000, seed=3, build=lambda t: None).tris
+    d = R.build_hlbvh_device(tris)
+    R.treelet_gpu_device(d)
+    nodes = R.records(d, L.BVHNODE).copy()
+    mats = S.random_mesh(8, seed=3).mats
+    rnd, host, dev = _upload_both(tris, nodes, mats)
+    for k in R.DeviceScene.ARRAYS + ("meta",):
+        assert host.read(k).tobytes() == dev.read(k).tobytes(), k
+    cam = S.parse_camera(S.RANDOM_MESH_CAMERA)
+    out = []
+    for sc in (host, dev):
+        st = rnd.new_state(96, 64)
+        rnd.render_frames(sc, cam, st, 4, 8, 3)
+        out.append((st.hist.cpu().numpy(), st.seeds_np()))
+    assert out[0][0].tobytes() == out[1][0].tobytes() and np.array_equal(out[0][1], out[1][1])
+    host.close()
+    dev.close()
+    rnd.close()
