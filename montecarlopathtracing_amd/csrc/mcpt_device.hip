@@ -1391,7 +1391,7 @@ __global__ void k_accumulate(f4 *colors, f4 *hist, int32_t *count, int64_t n, in
 // into the display's RGBA32F texture (openglapp.cpp:84).  Headless here: the
 // texture is a float4 buffer.  `1/2.2f` is the reference's constant (int 1 /
 // float 2.2f, folded at compile time); pow is OpenCL's, i.e. ocml's.
-__global__ void k_gamma_preview(const f4 *__restrict__ color, f4 *__restrict__ out, int64_t n) {
+__global__ void k_gamma_preview(const f4 *color, f4 *out, int64_t n) {  // out may be color (in place)
   const int64_t id = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (id >= n) return;
   constexpr float kInvGamma = 1 / 2.2f;

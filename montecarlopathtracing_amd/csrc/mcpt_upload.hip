@@ -17,7 +17,7 @@
 //    records with their Cramer minors.
 // Large ranges split level by level with workgroup-local bins merged by
 // atomics (min/max and counts: order-free); ranges of <= kSmall leaves are
-// finished by one workgroup each.  Compiled with the host's float semantics
+// finished by one wave each, in LDS.  Compiled with the host's float semantics
 // (-ffp-contract=off, IEEE division): Makefile BUILDFLAGS.
 #include <hip/hip_runtime.h>
 #include <hipcub/hipcub.hpp>
@@ -43,7 +43,7 @@ namespace {
 
 using mcpt::kEmptySlot4;
 constexpr int NB = 32;                 // mcpt_sah.cpp split(): bins per axis
-constexpr int kSmall = 2048;           // ranges at most this long: one workgroup builds the subtree
+constexpr int kSmall = 1024;           // ranges at most this long: one wave builds the subtree (k_small)
 constexpr double C_STEP = 1.0, C_TRI = 1.7;  // mcpt_sah.cpp collapse costs (MCPT_COLLAPSE_CTRI)
 
 __device__ __host__ inline float smin(float a, float b) { return (b < a) ? b : a; }  // std::min(a, b)
@@ -274,35 +274,46 @@ __global__ void k_leaf_init(const mcpt_bvh_node *__restrict__ nodes, int64_t n, 
   owner[i] = 0;
 }
 
-// centroid bounds of the large ranges (owner slot >= 0); a wave whose lanes
-// share a slot reduces first
-__global__ void k_cbounds(const int32_t *__restrict__ idx, const float *__restrict__ cen, const int32_t *__restrict__ owner,
-                          const int32_t *__restrict__ slot_of, int64_t m, Split *sp) {
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  int32_t s = -1;
-  float c[3] = {0, 0, 0};
-  if (i < m) {
-    s = slot_of[owner[i]];
-    if (s >= 0) {
-      const int32_t it = idx[i];
-      for (int a = 0; a < 3; ++a) c[a] = cen[3 * it + a];
+// centroid bounds of the large ranges (owner slot >= 0): a workgroup takes
+// a chunk of kBinChunk positions and reduces the chunk's first slot in
+// registers, then one atomic per wave into LDS and one per workgroup into
+// the slot (a chunk's other slots, where ranges meet, go straight to global)
+constexpr int kBinChunk = 4096;
+__global__ __launch_bounds__(256) void k_cbounds(const int32_t *__restrict__ idx, const float *__restrict__ cen,
+                                                 const int32_t *__restrict__ owner, const int32_t *__restrict__ slot_of,
+                                                 int64_t m, Split *sp) {
+  __shared__ uint32_t lmn[3], lmx[3];
+  __shared__ int32_t s_first;
+  const int64_t c0 = (int64_t)blockIdx.x * kBinChunk;
+  if (threadIdx.x == 0) s_first = c0 < m ? slot_of[owner[c0]] : -1;
+  if (threadIdx.x < 3) lmn[threadIdx.x] = 0xFFFFFFFFu, lmx[threadIdx.x] = 0u;
+  __syncthreads();
+  const int32_t sf = s_first;
+  uint32_t mn[3] = {0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu}, mx[3] = {0u, 0u, 0u};
+  for (int64_t i = c0 + threadIdx.x; i < min(c0 + kBinChunk, m); i += blockDim.x) {
+    const int32_t s = slot_of[owner[i]];
+    if (s < 0) continue;
+    const float *c = cen + 3 * (size_t)idx[i];
+    for (int a = 0; a < 3; ++a) {
+      const uint32_t o = f2o(c[a]);
+      if (s == sf)
+        mn[a] = min(mn[a], o), mx[a] = max(mx[a], o);
+      else
+        atomicMin(&sp[s].cmin[a], o), atomicMax(&sp[s].cmax[a], o);
     }
   }
-  const int32_t s0 = __shfl(s, 0, 64);
-  const bool uniform = __all(s == s0);
-  if (uniform) {
-    if (s0 < 0) return;
-    uint32_t mn[3], mx[3];
-    for (int a = 0; a < 3; ++a) mn[a] = mx[a] = f2o(c[a]);
-    for (int o = 32; o > 0; o >>= 1)
-      for (int a = 0; a < 3; ++a) {
-        mn[a] = min(mn[a], (uint32_t)__shfl_xor((int)mn[a], o, 64));
-        mx[a] = max(mx[a], (uint32_t)__shfl_xor((int)mx[a], o, 64));
-      }
-    if ((threadIdx.x & 63) == 0)
-      for (int a = 0; a < 3; ++a) atomicMin(&sp[s0].cmin[a], mn[a]), atomicMax(&sp[s0].cmax[a], mx[a]);
-  } else if (s >= 0) {
-    for (int a = 0; a < 3; ++a) atomicMin(&sp[s].cmin[a], f2o(c[a])), atomicMax(&sp[s].cmax[a], f2o(c[a]));
+  if (sf < 0) return;  // uniform: no thread of this chunk has a large first slot
+  for (int o = 32; o > 0; o >>= 1)
+    for (int a = 0; a < 3; ++a) {
+      mn[a] = min(mn[a], (uint32_t)__shfl_xor((int)mn[a], o, 64));
+      mx[a] = max(mx[a], (uint32_t)__shfl_xor((int)mx[a], o, 64));
+    }
+  if ((threadIdx.x & 63) == 0)
+    for (int a = 0; a < 3; ++a) atomicMin(&lmn[a], mn[a]), atomicMax(&lmx[a], mx[a]);
+  __syncthreads();
+  if (threadIdx.x < 3) {
+    if (lmn[threadIdx.x] != 0xFFFFFFFFu) atomicMin(&sp[sf].cmin[threadIdx.x], lmn[threadIdx.x]);
+    if (lmx[threadIdx.x] != 0u) atomicMax(&sp[sf].cmax[threadIdx.x], lmx[threadIdx.x]);
   }
 }
 
@@ -312,7 +323,6 @@ __device__ inline int bin_of(float c, float cmin, float scale) {  // split(): mi
 
 // bins of the large ranges: a workgroup accumulates a chunk in LDS for the
 // chunk's first slot, other slots' elements go straight to global atomics
-constexpr int kBinChunk = 4096;
 __global__ __launch_bounds__(256) void k_bins(const int32_t *__restrict__ idx, const float *__restrict__ cen,
                                               const float *__restrict__ box, const int32_t *__restrict__ owner,
                                               const int32_t *__restrict__ slot_of, int64_t m,
@@ -495,131 +505,182 @@ __global__ void k_place(const int32_t *__restrict__ idx, const int32_t *__restri
 }
 
 // ------------------------------------------------------ small ranges
-// one workgroup per range of <= kSmall leaves builds its whole subtree,
-// splitting cooperatively; pending ranges on a stack in LDS
-constexpr int kWG = 256;
-__global__ __launch_bounds__(kWG) void k_small(const int32_t *__restrict__ list, uint32_t count, int32_t *idx,
-                                               int32_t *tmp, const float *__restrict__ cen,
-                                               const float *__restrict__ box, SahNode *nodes) {
-  __shared__ int32_t stk[kSmall];  // node ids (a range of s leaves never holds more than s pending)
-  __shared__ int32_t sp;
+// One wave per range of <= kSmall leaves builds its whole subtree in LDS:
+// the range's leaf indices are read once, every split of the subtree
+// partitions them in LDS (the global idx order is not needed afterwards),
+// pending ranges sit on an LDS stack.  Per node: centroid bounds by wave
+// reduction, the 3 x 32 bins by LDS atomics, split()'s sweep with one lane
+// per (axis, bin) candidate (sweep_wave), the stable partition by ballot.
+// Same result as split() (min / max are exact in any order; only the sign
+// of a zero bound can differ, and the costs use differences of bounds, so
+// signs of zero never reach them).
+struct PendRange {
+  int32_t x, lo, hi, depth;  // node id, local range, depth
+};
+constexpr int kStk = kSmall / 2;  // pending ranges are disjoint with >= 2 leaves each
+
+__device__ inline uint32_t lane_id() { return __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u)); }
+__device__ inline uint32_t lanes_below(uint64_t m) {
+  return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
+
+// split()'s sweep over LDS bins, one lane per (axis, bin k) candidate: the
+// left side is bins [0, k) (inclusive prefix of k-1), the right side
+// [k, NB) (inclusive suffix), the winner the least cost, ties to the
+// earlier candidate of split()'s order (axis ascending, bin descending)
+__device__ inline Choice sweep_wave(const uint32_t (*lb)[NB][6], const uint32_t (*lc)[NB], const float *cmin,
+                                    const float *cmax) {
+  const int lane = (int)lane_id(), j = lane & (NB - 1);
+  double best = DBL_MAX;
+  int best_ord = INT_MAX, best_left = 0;
+  for (int pass = 0; pass < 2; ++pass) {
+    const int a = (lane >> 5) + 2 * pass;
+    const int ac = a < 3 ? a : 2;
+    float pb[6], sb[6];
+    const uint32_t n = lc[ac][j];
+    for (int e = 0; e < 6; ++e) pb[e] = n ? o2f(lb[ac][j][e]) : ((e & 1) ? -FLT_MAX : FLT_MAX);
+    uint32_t pc = n, sc = n;
+    for (int e = 0; e < 6; ++e) sb[e] = pb[e];
+    for (int o = 1; o < NB; o <<= 1) {  // inclusive prefix / suffix within the 32-lane axis segment
+      uint32_t tp = __shfl_up(pc, o, NB), ts = __shfl_down(sc, o, NB);
+      float up[6], dn[6];
+      for (int e = 0; e < 6; ++e) up[e] = __shfl_up(pb[e], o, NB), dn[e] = __shfl_down(sb[e], o, NB);
+      if (j >= o) {
+        pc += tp;
+        grow6(pb, up);
+      }
+      if (j + o < NB) {
+        sc += ts;
+        grow6(sb, dn);
+      }
+    }
+    float lbx[6];
+    for (int e = 0; e < 6; ++e) lbx[e] = __shfl_up(pb[e], 1, NB);
+    const uint32_t lcnt = __shfl_up(pc, 1, NB);
+    const float ext = cmax[ac] - cmin[ac];
+    if (a < 3 && ext > 0 && j >= 1 && lcnt && sc) {
+      const double c = area6(lbx) * (double)lcnt + area6(sb) * (double)sc;
+      const int ord = a * NB + (NB - 1 - j);
+      if (c < best || (c == best && ord < best_ord)) best = c, best_ord = ord, best_left = (int)lcnt;
+    }
+  }
+  for (int o = 32; o > 0; o >>= 1) {
+    const double c = __shfl_xor(best, o, 64);
+    const int ord = __shfl_xor(best_ord, o, 64), left = __shfl_xor(best_left, o, 64);
+    if (c < best || (c == best && ord < best_ord)) best = c, best_ord = ord, best_left = left;
+  }
+  Choice ch{-1, -1, 0};
+  if (best_ord != INT_MAX) ch.axis = best_ord / NB, ch.bin = NB - 1 - best_ord % NB, ch.left = best_left;
+  return ch;
+}
+
+__global__ __launch_bounds__(64) void k_small(const int32_t *__restrict__ list, uint32_t count,
+                                              const int32_t *__restrict__ idx, const float *__restrict__ cen,
+                                              const float *__restrict__ box, SahNode *nodes) {
+  __shared__ int32_t sidx[kSmall], stmp[kSmall];
+  __shared__ PendRange stk[kStk];
   __shared__ uint32_t lb[3][NB][6];
   __shared__ uint32_t lc[3][NB];
-  __shared__ uint32_t cb[6];
-  __shared__ Choice ch_s;
-  __shared__ uint32_t scan[kWG];
   if (blockIdx.x >= count) return;
-  const int t = threadIdx.x;
-  if (t == 0) {
-    stk[0] = list[blockIdx.x];
-    sp = 1;
+  const int lane = (int)threadIdx.x;
+  const int32_t x0 = list[blockIdx.x];
+  const int32_t lo0 = nodes[x0].lo, r0 = nodes[x0].hi - lo0;
+  // a leaf: its box, no children, its item (lane e writes word e of the record)
+  auto leaf = [&](int32_t x, int32_t it) {
+    if (lane < 6) nodes[x].box[lane] = box[6 * (size_t)it + lane];
+    if (lane == 6) nodes[x].left = -1;
+    if (lane == 7) nodes[x].right = -1;
+    if (lane == 8) nodes[x].item = it;
+  };
+  if (r0 == 1) {
+    leaf(x0, idx[lo0]);
+    return;
   }
+  for (int i = lane; i < r0; i += 64) sidx[i] = idx[lo0 + i];
+  if (lane == 0) stk[0] = PendRange{x0, 0, r0, nodes[x0].depth};
+  int sp = 1;
   __syncthreads();
-  for (;;) {
-    __syncthreads();
-    if (sp == 0) break;
-    const int32_t x = stk[sp - 1];
-    __syncthreads();
-    if (t == 0) --sp;
-    SahNode &N = nodes[x];
-    const int32_t lo = N.lo, hi = N.hi;
-    if (hi - lo == 1) {
-      if (t == 0) {
-        const int32_t it = idx[lo];
-        for (int k = 0; k < 6; ++k) N.box[k] = box[6 * (size_t)it + k];
-        N.left = N.right = -1;
-        N.item = it;
-      }
-      continue;
-    }
+  while (sp > 0) {
+    const PendRange R = stk[--sp];
+    const int32_t lo = R.lo, hi = R.hi;
     // centroid bounds
-    if (t < 6) cb[t] = (t & 1) ? 0u : 0xFFFFFFFFu;
-    for (int k = t; k < 3 * NB; k += kWG) {
+    float cmin[3], cmax[3];
+    for (int a = 0; a < 3; ++a) cmin[a] = FLT_MAX, cmax[a] = -FLT_MAX;
+    for (int i = lo + lane; i < hi; i += 64) {
+      const float *c = cen + 3 * (size_t)sidx[i];
+      for (int a = 0; a < 3; ++a) cmin[a] = smin(cmin[a], c[a]), cmax[a] = smax(cmax[a], c[a]);
+    }
+    for (int o = 32; o > 0; o >>= 1)
+      for (int a = 0; a < 3; ++a) {
+        cmin[a] = smin(cmin[a], __shfl_xor(cmin[a], o, 64));
+        cmax[a] = smax(cmax[a], __shfl_xor(cmax[a], o, 64));
+      }
+    // bins
+    for (int k = lane; k < 3 * NB; k += 64) {
       const int a = k / NB, j = k % NB;
       for (int e = 0; e < 6; ++e) lb[a][j][e] = (e & 1) ? 0u : 0xFFFFFFFFu;
       lc[a][j] = 0;
     }
     __syncthreads();
-    for (int i = lo + t; i < hi; i += kWG) {
-      const float *c = cen + 3 * (size_t)idx[i];
-      for (int a = 0; a < 3; ++a) atomicMin(&cb[2 * a], f2o(c[a])), atomicMax(&cb[2 * a + 1], f2o(c[a]));
-    }
-    __syncthreads();
-    float cmin[3], cmax[3];
-    for (int a = 0; a < 3; ++a) cmin[a] = o2f(cb[2 * a]), cmax[a] = o2f(cb[2 * a + 1]);
-    for (int i = lo + t; i < hi; i += kWG) {
-      const int32_t it = idx[i];
+    for (int i = lo + lane; i < hi; i += 64) {
+      const int32_t it = sidx[i];
       const float *bx = box + 6 * (size_t)it;
+      uint32_t ob[6];
+      for (int e = 0; e < 6; ++e) ob[e] = f2o(bx[e]);
       for (int a = 0; a < 3; ++a) {
         const float ext = cmax[a] - cmin[a];
         if (!(ext > 0)) continue;
         const int k = bin_of(cen[3 * (size_t)it + a], cmin[a], NB / ext);
-        for (int e = 0; e < 6; ++e) (e & 1) ? atomicMax(&lb[a][k][e], f2o(bx[e])) : atomicMin(&lb[a][k][e], f2o(bx[e]));
+        for (int e = 0; e < 6; ++e) (e & 1) ? atomicMax(&lb[a][k][e], ob[e]) : atomicMin(&lb[a][k][e], ob[e]);
         atomicAdd(&lc[a][k], 1u);
       }
     }
     __syncthreads();
-    if (t == 0) {
-      float bb[3][NB][6];
-      uint32_t bc[3][NB];
-      for (int a = 0; a < 3; ++a)
-        for (int k = 0; k < NB; ++k) {
-          bc[a][k] = lc[a][k];
-          for (int e = 0; e < 6; ++e) bb[a][k][e] = bc[a][k] ? o2f(lb[a][k][e]) : ((e & 1) ? -FLT_MAX : FLT_MAX);
-        }
-      ch_s = sweep(bb, bc, cmin, cmax);
-    }
-    __syncthreads();
-    const Choice ch = ch_s;
+    const Choice ch = sweep_wave(lb, lc, cmin, cmax);
     int32_t mid = (lo + hi) / 2;
     if (ch.axis >= 0) {
-      const int32_t part = (int32_t)(lo + ch.left);
+      const int32_t part = lo + (int32_t)ch.left;
       if (part > lo && part < hi) mid = part;
-      // stable partition, kWG elements per step: block scan of the flags
+      // stable partition into stmp, 64 leaves per step
       const float cm = cmin[ch.axis], scale = NB / (cmax[ch.axis] - cmin[ch.axis]);
-      int32_t nl = 0, nr = 0;  // placed so far (uniform)
-      for (int base = lo; base < hi; base += kWG) {
-        const int i = base + t;
-        int32_t it = 0;
-        uint32_t f = 0;
-        if (i < hi) {
-          it = idx[i];
-          f = bin_of(cen[3 * (size_t)it + ch.axis], cm, scale) < ch.bin;
-        }
-        scan[t] = f;
-        __syncthreads();
-        for (int o = 1; o < kWG; o <<= 1) {  // inclusive Hillis-Steele scan
-          const uint32_t v = t >= o ? scan[t - o] : 0u;
-          __syncthreads();
-          scan[t] += v;
-          __syncthreads();
-        }
-        const uint32_t inc = scan[t], total = scan[kWG - 1];
-        if (i < hi) {
-          const int32_t before_l = (int32_t)(inc - f);
-          const int32_t p = f ? lo + nl + before_l : part + nr + (t - before_l);
-          tmp[p] = it;
-        }
-        const int32_t chunk = min(kWG, hi - base);
-        nl += (int32_t)total;
-        nr += chunk - (int32_t)total;
-        __syncthreads();
+      int32_t nl = 0, nr = 0;
+      for (int base = lo; base < hi; base += 64) {
+        const int i = base + lane;
+        const bool valid = i < hi;
+        const int32_t it = valid ? sidx[i] : 0;
+        const bool f = valid && bin_of(cen[3 * (size_t)it + ch.axis], cm, scale) < ch.bin;
+        const uint64_t bal = __ballot(f);
+        const int32_t before = (int32_t)lanes_below(bal), tot = (int32_t)__popcll(bal);
+        if (valid) stmp[f ? lo + nl + before : part + nr + (lane - before)] = it;
+        nl += tot;
+        nr += min(64, hi - base) - tot;
       }
-      for (int i = lo + t; i < hi; i += kWG) idx[i] = tmp[i];
+      __syncthreads();
+      for (int i = lo + lane; i < hi; i += 64) sidx[i] = stmp[i];
+      __syncthreads();
     }
-    const int32_t lb_ = x + 1, rb_ = x + 2 * (mid - lo);
-    if (t == 0) {
-      N.left = lb_;
-      N.right = rb_;
-      N.item = -1;
-      nodes[lb_].lo = lo, nodes[lb_].hi = mid, nodes[lb_].depth = N.depth + 1;
-      nodes[rb_].lo = mid, nodes[rb_].hi = hi, nodes[rb_].depth = N.depth + 1;
-      stk[sp] = rb_;
-      stk[sp + 1] = lb_;
-      sp += 2;
+    const int32_t lx = R.x + 1, rx = R.x + 2 * (mid - lo);
+    if (lane == 0) {
+      nodes[R.x].left = lx;
+      nodes[R.x].right = rx;
+      nodes[R.x].item = -1;
+      nodes[lx].lo = lo0 + lo, nodes[lx].hi = lo0 + mid, nodes[lx].depth = R.depth + 1;
+      nodes[rx].lo = lo0 + mid, nodes[rx].hi = lo0 + hi, nodes[rx].depth = R.depth + 1;
+    }
+    // right pushed first: the left child is split next
+    if (hi - mid == 1)
+      leaf(rx, sidx[mid]);
+    else {
+      if (lane == 0) stk[sp] = PendRange{rx, mid, hi, R.depth + 1};
+      ++sp;
+    }
+    if (mid - lo == 1)
+      leaf(lx, sidx[lo]);
+    else {
+      if (lane == 0) stk[sp] = PendRange{lx, lo, mid, R.depth + 1};
+      ++sp;
     }
     __syncthreads();
-    __threadfence_block();
   }
 }
 
@@ -649,15 +710,20 @@ __global__ void k_large_slots(const int32_t *__restrict__ list, uint32_t count, 
 // depth of every node as a sort key (ids ascending within a depth after a stable sort)
 __global__ void k_depth_keys(const SahNode *__restrict__ sn, int64_t nb, uint32_t *key, int32_t *id, uint32_t *maxd) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= nb) return;
-  key[i] = (uint32_t)sn[i].depth;
-  id[i] = (int32_t)i;
-  atomicMax(maxd, (uint32_t)sn[i].depth);
+  uint32_t w = 0;  // every lane stays for the wave reduction: one atomic per wave
+  if (i < nb) {
+    w = (uint32_t)sn[i].depth;
+    key[i] = w;
+    id[i] = (int32_t)i;
+  }
+  for (int o = 32; o > 0; o >>= 1) w = max(w, (uint32_t)__shfl_xor((int)w, o, 64));
+  if ((threadIdx.x & 63) == 0) atomicMax(maxd, w);
 }
-__global__ void k_depth_hist(const uint32_t *__restrict__ key, int64_t nb, uint32_t *hist) {
+// first position of every depth in the sorted keys (every depth 0..max occurs)
+__global__ void k_depth_starts(const uint32_t *__restrict__ key, int64_t nb, uint32_t *start) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= nb) return;
-  atomicAdd(&hist[key[i]], 1u);
+  if (i == 0 || key[i] != key[i - 1]) start[key[i]] = (uint32_t)i;
 }
 
 // collapse DP (mcpt_sah.cpp build_sah4): f[x][1..4], cut[x][1..4], wide[x]
@@ -1125,7 +1191,7 @@ int build_scene_device(const mcpt_triangle *tris, int64_t n, const mcpt_bvh_node
   while (n_large > 0) {
     hipLaunchKernelGGL(k_large_slots, dim3(n_large), dim3(64), 0, st, large, n_large, 0, slot_of, sp, bins);
     UP_OK(hipGetLastError());
-    hipLaunchKernelGGL(k_cbounds, dim3(nblk(m, 256)), dim3(256), 0, st, idx, cen, own, slot_of, m, sp);
+    hipLaunchKernelGGL(k_cbounds, dim3(nblk(m, kBinChunk)), dim3(256), 0, st, idx, cen, own, slot_of, m, sp);
     UP_OK(hipGetLastError());
     hipLaunchKernelGGL(k_bins, dim3(nblk(m, kBinChunk)), dim3(256), 0, st, idx, cen, lbox, own, slot_of, m, sp, bins);
     UP_OK(hipGetLastError());
@@ -1151,7 +1217,7 @@ int build_scene_device(const mcpt_triangle *tris, int64_t n, const mcpt_bvh_node
   uint32_t n_small_h = 0;
   if (int rc = d2h(&n_small_h, n_small, 1, st)) return rc;
   if (n_small_h > 0) {
-    hipLaunchKernelGGL(k_small, dim3(n_small_h), dim3(kWG), 0, st, small, n_small_h, idx, idx2, cen, lbox, sn);
+    hipLaunchKernelGGL(k_small, dim3(n_small_h), dim3(64), 0, st, small, n_small_h, idx, cen, lbox, sn);
     UP_OK(hipGetLastError());
   }
   // the binary SAH tree by depth (stable radix sort of the depths), then
@@ -1179,13 +1245,13 @@ int build_scene_device(const mcpt_triangle *tris, int64_t n, const mcpt_bvh_node
     UP_OK(hipcub::DeviceRadixSort::SortPairs(tmp, bytes, dkey, dkey2, ids, ids2, (int)nb, 0, end_bit, st));
   }
   UP_OK(S.alloc(&hist, maxd_h + 1));
-  UP_OK(hipMemsetAsync(hist, 0, (maxd_h + 1) * sizeof(uint32_t), st));
-  hipLaunchKernelGGL(k_depth_hist, dim3(nblk(nb, 256)), dim3(256), 0, st, dkey2, nb, hist);
+  hipLaunchKernelGGL(k_depth_starts, dim3(nblk(nb, 256)), dim3(256), 0, st, dkey2, nb, hist);
   UP_OK(hipGetLastError());
-  std::vector<uint32_t> hist_h(maxd_h + 1);
-  if (int rc = d2h(hist_h.data(), hist, maxd_h + 1, st)) return rc;
   std::vector<uint32_t> doff(maxd_h + 2, 0);
-  for (uint32_t d = 0; d <= maxd_h; ++d) doff[d + 1] = doff[d] + hist_h[d];
+  if (int rc = d2h(doff.data(), hist, maxd_h + 1, st)) return rc;
+  doff[maxd_h + 1] = (uint32_t)nb;
+  std::vector<uint32_t> hist_h(maxd_h + 1);
+  for (uint32_t d = 0; d <= maxd_h; ++d) hist_h[d] = doff[d + 1] - doff[d];
   DP *dp = nullptr;
   UP_OK(S.alloc(&dp, nb));
   for (int64_t d = maxd_h; d >= 0; --d) {

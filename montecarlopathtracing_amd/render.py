@@ -319,6 +319,9 @@ class Renderer:
         color = color.contiguous()
         if out is None:
             out = torch.empty_like(color)
+        elif (out.dtype != torch.float32 or not out.is_cuda or out.device != color.device
+              or not out.is_contiguous() or out.numel() != color.numel()):
+            raise L.MCPTError("gamma_preview: out must be a contiguous float32 CUDA tensor the size of color")
         L.check(L.lib().mcpt_gamma_preview(self.ctx, L.ptr(color), L.ptr(out), color.numel() // 4, _stream()))
         return out.view(-1, 4)
 

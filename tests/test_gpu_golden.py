@@ -258,6 +258,12 @@ def test_gamma_preview_is_opencl_pow(rnd):
     assert np.array_equal(sp, np.power(col[:, :3].ravel()[np.isin(col[:, :3].ravel(), [0.0, 1.0, np.inf])], 1.0))
     rnd.gamma_preview(dev, out=dev)                                # in place
     assert np.array_equal(dev.cpu().numpy().view(np.int32), out.view(np.int32))
+    for bad in (torch.empty(dev.numel() - 4, device=rnd.device),   # too small
+                torch.empty(dev.shape[::-1], device=rnd.device).t(),  # strided
+                torch.empty(dev.shape, dtype=torch.float64, device=rnd.device),
+                torch.empty(dev.shape)):                           # host
+        with pytest.raises(L.MCPTError):
+            rnd.gamma_preview(dev, out=bad)
 
 
 def test_cli_runs(tmp_path):

@@ -80,16 +80,41 @@ def main():
                 tg_same = bool(rc == 0 and np.array_equal(R.records(dn, L.BVHNODE).view(np.uint8), ref.view(np.uint8)))
         except ImportError:
             pass
+        deployed = data.with_nodes(R.records(dn, L.BVHNODE).copy())
         rnd = R.Renderer(0)
         t0 = time.perf_counter()
-        sc = rnd.upload(data)
+        sc = rnd.upload(deployed)
         torch.cuda.synchronize()
         t_up = time.perf_counter() - t0
+        # the same structures built on the GPU from the tree in HBM (mcpt_scene_upload_device)
+        dn = R.build_hlbvh_device(dt)
+        R.treelet_gpu_device(dn)
+        sc2 = rnd.upload((dt, dn, data.mats))  # warm (hipCUB kernels, allocator)
+        sc2.close()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        sc2 = rnd.upload((dt, dn, data.mats))
+        torch.cuda.synchronize()
+        t_upd = time.perf_counter() - t0
+        same_up = all(sc.read(k).tobytes() == sc2.read(k).tobytes() for k in R.DeviceScene.ARRAYS + ("meta",))
+        # the whole GPU pipeline from triangles in HBM: HLBVH + GPU treelet pass + upload
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        dn = R.build_hlbvh_device(dt)
+        R.treelet_gpu_device(dn)
+        sc3 = rnd.upload((dt, dn, data.mats))
+        torch.cuda.synchronize()
+        t_pipe = time.perf_counter() - t0
+        sc3.close()
+        sc2.close()
         sc.close()
         rnd.close()
         print(json.dumps({"workload": wl, "triangles": len(tris), "hlbvh_host_s": round(t_host, 4),
                           "hlbvh_gpu_s": round(t_dev, 4), "gpu_equals_host": same,
-                          "scene_upload_s": round(t_up, 4), "treelet_gpu_s": round(t_tl, 4),
+                          "scene_upload_s": round(t_up, 4), "scene_upload_device_s": round(t_upd, 4),
+                          "upload_device_equals_host": same_up,
+                          "gpu_pipeline_s (hlbvh + treelet kernel pass + upload)": round(t_pipe, 4),
+                          "treelet_gpu_s": round(t_tl, 4),
                           "treelet_cpu_oracle_s": None if t_tl_cpu is None else round(t_tl_cpu, 4),
                           "treelet_gpu_equals_oracle": tl_same,
                           "treelet_gpu_kernel_pass_s": round(t_tg, 4),

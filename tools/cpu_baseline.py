@@ -28,6 +28,11 @@ def main():
             data, camj = scenes.cbox(), scenes.CBOX_CAM
         else:
             data, camj = bench.load_scene(name)
+            if data.nodes is None:  # C5: the deployed tree, built on the GPU
+                from montecarlopathtracing_amd import render as R
+                from montecarlopathtracing_amd import _lib as L
+                dn = R.build_hlbvh_device(R.to_device(data.tris, 0))
+                data = data.with_nodes(R.records(R.treelet_gpu_device(dn), L.BVHNODE).copy())
         cb = bench.cpu_baseline(data, S.parse_camera(camj), wl["h"], label=name)
         print(json.dumps({"workload": wl["desc"], "cpu_baseline": cb}), flush=True)
 

@@ -34,7 +34,7 @@ def main():
     data, camj = bench.load_scene(a.workload)
     cam = S.parse_camera(camj)
     rnd = R.Renderer(0)
-    dsc = rnd.upload(data)
+    dsc, _ = bench.upload_scene(rnd, data)
     dsc.schedule = L.SCHED_PAIRED
     if a.tuning:
         rnd.set_tuning(**{k: int(v) for k, v in (x.split("=") for x in a.tuning.split(","))})

@@ -57,7 +57,7 @@ def main():
     data, camj = bench.load_scene(a.workload)
     cam = S.parse_camera(camj)
     rnd = R.Renderer(0)
-    dsc = rnd.upload(data)
+    dsc, _ = bench.upload_scene(rnd, data)
     dsc.schedule = L.SCHED_PAIRED if a.schedule == "paired" else L.SCHED_SINGLE
     st = rnd.new_state(w, h)
     combos = [(fpl, g, n) for n in (int(x) for x in a.stripes.split(",")) for fpl in (int(x) for x in a.fpl.split(","))
