@@ -433,7 +433,7 @@ def main():
                           "schedule": "paired" if dsc.schedule == L.SCHED_PAIRED else "single",
                           "shade_threshold": shade_th,
                           "fetch_threshold": rnd.get_tuning()["fetch_threshold"] or 1,
-                          "block_entries": rnd.get_tuning()["block_entries"] or 32,
+                          "block_entries": rnd.get_tuning()["block_entries"] or 8,
                           "frames_per_block": fpb, "search_tree_nodes": search_tree},
                "active_Msegments_per_s": round(segments * n / elapsed / 1e6, 2),
                "scene_build_gpu_s": None if build_s is None else round(build_s, 3),

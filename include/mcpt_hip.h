@@ -186,9 +186,9 @@ typedef struct mcpt_tuning {
   int32_t shade_threshold;  /* lanes waiting before the S phase runs, for 64
                                live lanes (32; scaled the same way)            */
   int32_t queue_chunk;      /* queue entries a wave claims per atomic (4)        */
-  int32_t block_entries;    /* auto frames-per-block: smallest block count that
-                               gives every resident lane this many queue entries
-                               (32)                                              */
+  int32_t block_entries;    /* auto frames-per-block: smallest block count (at
+                               least 2) that gives every resident lane this many
+                               queue entries (8)                                 */
   int32_t max_block_frames; /* auto frames-per-block upper bound (32)            */
   int32_t stack_window;     /* 0 auto (default), 1 the 32-entry LDS window with
                                a global spill, 2 the whole stack in LDS          */

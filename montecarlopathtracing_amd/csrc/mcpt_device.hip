@@ -147,6 +147,7 @@ struct mcpt_scene {
 
 constexpr int kQueues = 8;         // k_render work queues (at most): one per XCD (MI355X has 8)
 constexpr int kQueueStride = 32;   // u32 words between queue heads: one 128-B line each
+constexpr int kDefaultBlockEntries = 8;  // mcpt_tuning.block_entries = 0 (launch plan, below)
 constexpr int kHandoffWords = 4;   // seed, mean.xyzw, count in four tagged 8-B granules (two 16-B stores)
 constexpr int kMaxBlocksPerLaunch = 255;  // the hand-off tag's 8 bits of block index
 constexpr int kStatSlots = 24;
@@ -2194,9 +2195,13 @@ int mcpt_render_frames(mcpt_ctx *ctx, const mcpt_scene *scene, const mcpt_camera
   // block.  One launch runs many blocks of every pixel, block-major, so lanes
   // stay busy until the last block (no per-block drain of the GPU).
   // frames_per_launch <= 0: auto.  Blocks let the launch's tail shrink: the
-  // fewest blocks that give every resident lane `block_entries` queue entries
-  // (so the tail, where lanes run dry, is about 1/block_entries of the
-  // launch), frames split evenly over them, at most max_block_frames each.
+  // fewest blocks (at least 2) that give every resident lane `block_entries`
+  // queue entries (so the tail, where lanes run dry, is about
+  // 1/block_entries of the launch), frames split evenly over them, at most
+  // max_block_frames each.  Each block boundary costs a hand-off per pixel;
+  // with the packed hand-off, 8 entries and 2-3 blocks per call measured best
+  // (20-frame calls: C2 -2 %, C3 -11 %, C4 -1 %, C5 even against 32 entries;
+  // one block loses 2-7 % to the tail; profiles/r03_blocks.txt).
   // That needs several entries per lane in each block (>= 4): a pixel's next
   // block is then claimed long after its previous one started.  With fewer
   // (small images, strong-scaled ranks: about one pixel per lane) every block
@@ -2208,9 +2213,9 @@ int mcpt_render_frames(mcpt_ctx *ctx, const mcpt_scene *scene, const mcpt_camera
   if (fpl <= 0) {
     const int frames = std::max(p->frames, 1);
     const double per_block = (double)n_items / (double)(grid * 64);  // entries per lane per block
-    const int want = T.block_entries > 0 ? T.block_entries : 32;
+    const int want = T.block_entries > 0 ? T.block_entries : kDefaultBlockEntries;
     const int cap = T.max_block_frames > 0 ? T.max_block_frames : 32;
-    int nb = (int)std::ceil(want / std::max(per_block, 1e-9));
+    int nb = std::max(2, (int)std::ceil(want / std::max(per_block, 1e-9)));
     nb = std::max(1, std::min(nb, frames));
     fpl = (frames + nb - 1) / nb;
     if (per_block < 4.0) fpl = std::max(fpl, 4);

@@ -223,13 +223,13 @@ class Renderer:
         return sched, {k[0]: v for k, v in best.items()}
 
     def tune(self, scene, camera, state, max_depth, max_attempt, frames=64, trials=1, shade_thresholds=(32, 40, 48),
-             fetch_thresholds=(1, 8), block_entries=(8, 32), **kw):
+             fetch_thresholds=(1, 8), block_entries=(8, 16), **kw):
         """tune_schedule over the leaf-test schedule, the S-phase threshold
         (mcpt_tuning.shade_threshold) and then the fetch threshold
         (mcpt_tuning.fetch_threshold), then the block sizing
         (mcpt_tuning.block_entries): their best values differ by scene
-        (veach_mis: S 40, fetch 8, 8 entries; cbox: 32-40, 8, 32; the 10 M-triangle
-        soup: 32, 1, 32).  Every combination gives the same bits.  The
+        (round 2, 3-frame blocks: veach_mis S 40, fetch 8; cbox S 32-40, fetch 8;
+        the 10 M-triangle soup S 32, fetch 1).  Every combination gives the same bits.  The
         winner goes to scene.schedule and the renderer's tuning.  Returns
         (schedule, shade_threshold, {(schedule, shade, fetch, entries): best ms})."""
         if getattr(self, "_stats_on", False):
@@ -249,7 +249,7 @@ class Renderer:
             best[(sched, th, fe, be)] = min(best.get((sched, th, fe, be), ms), ms)
 
         fe0 = base["fetch_threshold"] or 1  # 0 = the default, 1
-        be0 = base["block_entries"] or 32   # 0 = the default, 32
+        be0 = base["block_entries"] or 8    # 0 = the default, 8
         try:
             for _ in range(int(trials)):
                 for th in ths:

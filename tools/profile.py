@@ -76,7 +76,7 @@ def run(tag, args):
     cfg = json.loads(line.splitlines()[-1])["config"]
     quiet = bench + ["--no-cpu", "--no-cache-off", "--schedule", cfg["schedule"], "--shade-threshold", str(cfg.get("shade_threshold", 32)),
                      "--fetch-threshold", str(cfg.get("fetch_threshold", 1)),
-                     "--block-entries", str(cfg.get("block_entries", 32))]
+                     "--block-entries", str(cfg.get("block_entries", 8))]
     sh(["rocprofv3", "--kernel-trace", "--stats", "--output-format", "csv", "-d", os.path.join(out, "trace"), "--"]
        + quiet, os.path.join(out, "trace.log"), 400)
     print("trace done", flush=True)
@@ -135,7 +135,7 @@ def summarize(tag):
     sched = bench["config"]["schedule"]
     quant = "true" if bench["config"].get("search_tree_nodes", "").startswith("64") else "false"
     # the render instantiation (PRIM = false), not the primary-hit pass (PRIM = true)
-    kname = r"k_render<0, false, (false|true), %s, %s, false>" % ("true" if sched == "paired" else "false", quant)
+    kname = r"k_render<0, false, (false|true), %s, %s, false, (false|true)>" % ("true" if sched == "paired" else "false", quant)
     trace = [r for r in csv.DictReader(open(trace_csv)) if re.search(kname, r["Kernel_Name"])]
     timed = trace[-1]
     timed_ms = (int(timed["End_Timestamp"]) - int(timed["Start_Timestamp"])) / 1e6
