@@ -2219,14 +2219,15 @@ int mcpt_render_frames(mcpt_ctx *ctx, const mcpt_scene *scene, const mcpt_camera
     nb = std::max(1, std::min(nb, frames));
     fpl = (frames + nb - 1) / nb;
     if (per_block < 4.0) fpl = std::max(fpl, 4);
-    // at most about one pixel per lane (strong-scaled ranks): nothing left to
+    // at most a few pixels per lane (strong-scaled ranks): little left to
     // balance but the pixels' own chains, so one block per pixel below 0.75
-    // pixels per lane and two up to 1.25 (C2 shares of 4 and 8 ranks, C4 of 8:
-    // 1-12 % faster than 4-frame blocks; tools/sweep.py --stripes --fpl)
+    // pixels per lane and two up to 2.5 (C2 shares of 4 and 8 ranks, C4 of 8:
+    // 1-12 % faster than 4-frame blocks; the C5 8-rank share, 2 pixels per
+    // lane: 4 % faster than 5-frame blocks; tools/sweep.py --stripes --fpl)
     const double per_slot = (double)n_items / ((double)std::max(per_cu, 1) * ctx->n_cu * 64);  // vs resident lanes
     if (per_slot < 0.75)
       fpl = frames;
-    else if (per_slot <= 1.25)
+    else if (per_slot <= 2.5)
       fpl = std::max(fpl, (frames + 1) / 2);
     fpl = std::max(1, std::min({fpl, cap, frames}));
   }
