@@ -194,11 +194,15 @@ constexpr bool kDebug = false;
 // primary ray every frame (rayGenerator.cl has no jitter), so its closest hit
 // is the same in every frame; k_render reads it instead of tracing segment 0.
 // nrm = the hit triangle's packed normal (material id bits in .w), t = the
-// closest-hit distance (kFltMax: miss).
+// closest-hit distance (kFltMax: miss), ray = the primary ray's per-pixel
+// part as gen_ray_px makes it: the direction's xyz (pinhole camera) or the
+// origin's xyz (camera_type 1); the rest of the ray is the same for every
+// pixel (LdsUniforms::ray_u), so a frame starts without generateRay's
+// arithmetic.
 struct __attribute__((aligned(16))) PrimHit {
   f4 nrm;
   float t;
-  int32_t pad[3];
+  float ray[3];
 };
 static_assert(sizeof(PrimHit) == 32, "32-B primary hit");
 // What a primary-hit cache was computed for: same scene, camera, image,
@@ -605,9 +609,8 @@ __device__ inline ShadeOut shade_hit(const mcpt_material *__restrict__ mats, con
       // glossy: the lobe coin (shade.cl:115), then the Phong lobe around the
       // mirror direction, else the diffuse lobe (shade.cl:139)
       const bool lobe = resample || (type == MCPT_GLOSSY && (lcg15(seed) & 0x00000001));
-      f4 axis = in.nrm;
-      if (lobe) axis = mirror_dir(in.nrm, in.d);
-      nd = random_dir(axis, seed);
+      const f4 mir = lobe ? mirror_dir(in.nrm, in.d) : in.nrm;  // the lobe's axis
+      nd = random_dir(mir, seed);
       if (lobe && cl_dot3(nd.xyz, in.nrm.xyz) <= 0) {  // rejected: draw again next call
         resample = true;
         r.pending = true;
@@ -618,10 +621,9 @@ __device__ inline ShadeOut shade_hit(const mcpt_material *__restrict__ mats, con
       no.w = as_f(td + 1);
       nd.w = in.d.w;
       // diffuse: color * kd * cos / 2pi; glossy: color * ks * pow(cos_r, Ns) * cos / 2pi
-      // (the mirror direction recomputed rather than kept live across the draw)
       f4 c;
       if (lobe)
-        c = color * kaks_of() * cl_pow(cl_dot3(nd.xyz, mirror_dir(in.nrm, in.d).xyz), Mp->Ns);
+        c = color * kaks_of() * cl_pow(cl_dot3(nd.xyz, mir.xyz), Mp->Ns);
       else
         c = color * kd_of();
       color = cl_div4(c * cl_dot3(nd.xyz, in.nrm.xyz), (float)(2 * kClPi));
@@ -735,8 +737,9 @@ struct __attribute__((aligned(16))) LdsUniforms {
   mcpt_camera cam;
   f4 cc;  // generateRay's 0.5 / tan(arg / 2) and W / H (cam_const)
   f4 root_min, root_max;
+  f4 ray_u;  // the primary ray's pixel-independent part: the origin (pinhole) or the direction (camera_type 1)
 };
-static_assert(sizeof(LdsUniforms) == 128, "LDS uniforms");
+static_assert(sizeof(LdsUniforms) == 144, "LDS uniforms");
 
 struct RenderArgs {
   mcpt_camera cam;
@@ -829,6 +832,9 @@ __global__ void __launch_bounds__(64, MCPT_WAVES_PER_SIMD) k_render(RenderArgs A
     U->cc = (f4){c0.distance, c0.ratio, 0.0f, 0.0f};
     U->root_min = S.root_min;
     U->root_max = S.root_max;
+    f4 o0, d0;  // the pixel-independent part of every primary ray (PrimHit)
+    gen_ray_px(A.cam, c0, 0u, 0u, (uint32_t)A.W, (uint32_t)A.H, o0, d0);
+    U->ray_u = A.cam.camera_type == 0 ? o0 : d0;
   }
   const mcpt_material *mats = S.mats;
   if (A.lds_mats) {
@@ -858,7 +864,6 @@ __global__ void __launch_bounds__(64, MCPT_WAVES_PER_SIMD) k_render(RenderArgs A
     cc.distance = c4.x;
     cc.ratio = c4.y;
     gen_ray_px(U->cam, cc, pxy & 0xFFFFu, pxy >> 16, (uint32_t)A.W, (uint32_t)A.H, o, d);
-    color = (f4){1.0f, 1.0f, 1.0f, 1.0f};
   };
   // path / traversal state (declared with the pixel state below)
   f3 rinv = (f3){0.0f, 0.0f, 0.0f};
@@ -883,18 +888,30 @@ __global__ void __launch_bounds__(64, MCPT_WAVES_PER_SIMD) k_render(RenderArgs A
     else
       cur = kDone;
   };
-  // a frame's first segment: the primary ray's hit is the same every frame
-  // (k_primary computed it once), so the lane goes straight to S with it
+  // a frame's first segment: the primary ray and its hit are the same every
+  // frame (the primary-hit pass computed them once), so the lane takes both
+  // from the pixel's record and goes straight to S
   auto begin_frame = [&]() {
+    color = (f4){1.0f, 1.0f, 1.0f, 1.0f};
     if (A.prim) {
-      const PrimHit *ph = A.prim + ((size_t)(pxy >> 16) * (size_t)A.W + (pxy & 0xFFFFu));
-      best_nrm = ph->nrm;
-      best_t = ph->t;
+      const uint32_t pid = (pxy >> 16) * (uint32_t)A.W + (pxy & 0xFFFFu);
+      const f4 *ph = reinterpret_cast<const f4 *>(A.prim + pid);
+      const f4 h0 = ph[0], h1 = ph[1];  // nrm | t, ray xyz
+      const f4 u = U->ray_u;
+      const f4 v = (f4){h1.y, h1.z, h1.w, 0.0f};
+      const bool pin = U->cam.camera_type == 0;
+      o = pin ? u : v;
+      d = pin ? v : u;
+      o.w = as_f(0);
+      d.w = as_f((int32_t)pid);  // gen_ray_px: idy * w + idx
+      best_nrm = h0;
+      best_t = h1.x;
       t2 = kFltMax;
       ref = LIT;
       sp = 0;
       cur = kDone;
     } else {
+      primary();
       begin_segment();
     }
   };
@@ -1003,7 +1020,6 @@ __global__ void __launch_bounds__(64, MCPT_WAVES_PER_SIMD) k_render(RenderArgs A
         if (ready) {
           lst = kBusy;
           f = 0;
-          primary();
           begin_frame();
         }
       }
@@ -1181,7 +1197,8 @@ __global__ void __launch_bounds__(64, MCPT_WAVES_PER_SIMD) k_render(RenderArgs A
         PrimHit h;
         h.nrm = best_t < kFltMax ? best_nrm : (f4){0.0f, 0.0f, 0.0f, 0.0f};
         h.t = best_t;
-        h.pad[0] = h.pad[1] = h.pad[2] = 0;
+        const f4 v = U->cam.camera_type == 0 ? d : o;
+        h.ray[0] = v.x, h.ray[1] = v.y, h.ray[2] = v.z;
         A.prim_out[(size_t)(pxy >> 16) * (size_t)A.W + (pxy & 0xFFFFu)] = h;
         lst = kNeed;
       } else if (in_s) {
@@ -1217,10 +1234,7 @@ __global__ void __launch_bounds__(64, MCPT_WAVES_PER_SIMD) k_render(RenderArgs A
           if (A.frame_begin + f0 + f <= A.max_attempt) (void)accumulate_one(color, hist, cnt, A.max_attempt);
           ++f;
           const int32_t fend = min(A.fpl, A.frames - f0);
-          if (f < fend) {
-            primary();
-            fresh = true;
-          }
+          fresh = f < fend;
           if (f == fend) {  // block complete: write back, fetch another next iteration
             const int32_t pid = (int32_t)(pxy >> 16) * A.W + (int32_t)(pxy & 0xFFFFu);
             if (blk + 1 < A.blocks) {  // publish for the lane that takes the next block
@@ -1341,7 +1355,8 @@ __global__ void __launch_bounds__(64) k_primary(RenderArgs A, PrimHit *out) {
   PrimHit h;
   h.nrm = tr.tri >= 0 ? A.S.tris[tr.tri].nrm : (f4){0.0f, 0.0f, 0.0f, 0.0f};
   h.t = tr.t;
-  h.pad[0] = h.pad[1] = h.pad[2] = 0;
+  const f4 v = A.cam.camera_type == 0 ? d : o;
+  h.ray[0] = v.x, h.ray[1] = v.y, h.ray[2] = v.z;
   out[(size_t)y * A.W + x] = h;
 }
 

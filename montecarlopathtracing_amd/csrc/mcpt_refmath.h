@@ -49,12 +49,20 @@ __device__ inline f4 cl_cross(f4 a, f4 b) {
   r.w = 0.0f;
   return r;
 }
-// normalize(float4): opencl.bc _Z9normalizeDv4_f
+// normalize(float4): opencl.bc _Z9normalizeDv4_f, with two steps reordered
+// for fewer instructions on the common path, same value for every input:
+//  * the all-zero test (return p) moved inside the small-l2 branch: an
+//    all-zero p has l2 = +0 and reaches it, any other p returns from the
+//    same arithmetic either way;
+//  * ocml's rsqrt scales an argument below 2^-126 before v_rsq_f32; l2 is
+//    never below 2^-126 there (a non-zero p rescaled by 2^86 has a
+//    component of at least 2^-63, the inf branch ends at >= 1 or NaN), so
+//    its v_rsq_f32 is taken directly.
 __device__ inline f4 cl_normalize(f4 p) {
-  if (p.x == 0.0f && p.y == 0.0f && p.z == 0.0f && p.w == 0.0f) return p;
   float l2 = cl_dot4(p, p);
   f4 q = p;
   if (l2 < 0x1p-126f) {
+    if (p.x == 0.0f && p.y == 0.0f && p.z == 0.0f && p.w == 0.0f) return p;
     q = p * 0x1p86f;
     l2 = cl_dot4(q, q);
   } else if (l2 == __builtin_inff()) {
@@ -70,7 +78,7 @@ __device__ inline f4 cl_normalize(f4 p) {
       l2 = cl_dot4(q, q);
     }
   }
-  return q * __ocml_rsqrt_f32(l2);
+  return q * __builtin_amdgcn_rsqf(l2);
 }
 // OpenCL's default sqrt: llvm.sqrt with !fpmath 3.0, which gfx950 lowers to
 // v_sqrt_f32 with denormal range scaling (x < 2^-126: sqrt(x * 2^32) * 2^-16).
@@ -175,7 +183,7 @@ __device__ inline f4 random_dir(f4 n, uint32_t &seed) {
   n.w = 0;
   float phi = random_phi(lcg15(seed));
   float u = lcg15(seed) * 1.0f * 0x1p-15f;  // = the 2.5-ulp x / 32768: both exact for x < 2^24
-  float s = cl_sqrt(u);
+  float s = __builtin_amdgcn_sqrtf(u);        // = cl_sqrt(u): u is 0 or >= 2^-15, never scaled
   float sin_phi, cos_phi;
   sincos_small(phi, sin_phi, cos_phi);
   f4 a1, a2;

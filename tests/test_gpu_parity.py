@@ -295,6 +295,37 @@ def test_render_frames_chunked_and_striped_bitexact(rnd):
 
 
 @needs_ref
+@pytest.mark.parametrize("cache", [2, 1])
+def test_orthographic_camera_render_bitexact(rnd, cache):
+    """rayGenerator.cl's second camera (camera_type 1: every ray along the view
+    direction, origins spread over the image plane; parseCamera never makes it,
+    a C host can).  A frame started from the primary-hit record takes the
+    per-pixel origin from the record and the shared direction from the launch:
+    the reference's bits, cache off and on."""
+    data = scenes.mis()
+    cam = S.parse_camera(scenes.MIS_CAM).copy()
+    cam["camera_type"] = 1
+    cam["arg"] = np.float32(9.5)  # the image plane's width in scene units
+    w, h, depth, frames, attempt = 40, 32, 6, 4, 8
+    seeds = R.default_seeds(w * h)
+    rh, rc, rs = refgpu.render(data, cam, w, h, depth, frames, attempt, seeds)
+    dsc = rnd.upload(data)
+    try:
+        rnd.set_tuning(primary_cache=cache)
+        st = rnd.new_state(w, h, seeds)
+        rnd.render_frames(dsc, cam, st, depth, attempt, frames)
+        assert rnd.stats()["primary_cache"] == (2 if cache == 1 else 0)
+        torch.cuda.synchronize()
+        assert_bits_equal(st.count.cpu().numpy(), rc, "count")
+        assert_bits_equal(st.seeds_np(), rs, "seeds")
+        assert_bits_equal(st.hist.cpu().numpy(), rh, "hist")
+        assert (rc > 0).mean() > 0.05  # some rays reach lit surfaces (measured 0.13)
+    finally:
+        rnd.set_tuning()
+        dsc.close()
+
+
+@needs_ref
 @pytest.mark.parametrize("mode", [L.MODE_EXACT, L.MODE_NOPRUNE])
 @pytest.mark.parametrize("name,getter,camjson", [("cbox", scenes.cbox, scenes.CBOX_CAM), ("mis", scenes.mis, scenes.MIS_CAM)])
 def test_primary_hit_cache_bitexact(rnd, name, getter, camjson, mode):
