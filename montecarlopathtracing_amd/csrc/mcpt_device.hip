@@ -579,16 +579,16 @@ struct ShadeOut {
 // (diffuse, and glossy either lobe), instead of holding the whole wave in
 // the loop.  G = false: a scene without glossy materials (C2's diffuse-only
 // override, C5): the diffuse lobe alone, no coin, never pending.
-template <bool G = true>
-__device__ inline ShadeOut shade_hit(const mcpt_material *__restrict__ mats, const ShadeIn &in, f4 color,
-                                     uint32_t &seed, int max_depth, bool &resample) {
+template <bool G = true, class Mat = const mcpt_material>
+__device__ inline ShadeOut shade_hit(Mat *__restrict__ mats, const ShadeIn &in, f4 color, uint32_t &seed,
+                                     int max_depth, bool &resample) {
   ShadeOut r;
   r.bad = false;
   r.new_ray = true;
   r.pending = false;
   // material fields are read where they are used (the table is in LDS): the
   // draw below keeps fewer values live
-  const mcpt_material *__restrict__ Mp = mats + in.mat;
+  Mat *__restrict__ Mp = mats + in.mat;
   const int32_t type = Mp->type;
   auto kd_of = [&]() { return (f4){Mp->kd[0], Mp->kd[1], Mp->kd[2], Mp->kd[3]}; };
   auto kaks_of = [&]() { return (f4){Mp->ka_ks[0], Mp->ka_ks[1], Mp->ka_ks[2], Mp->ka_ks[3]}; };
@@ -836,11 +836,11 @@ __global__ void __launch_bounds__(64, MCPT_WAVES_PER_SIMD) k_render(RenderArgs A
     gen_ray_px(A.cam, c0, 0u, 0u, (uint32_t)A.W, (uint32_t)A.H, o0, d0);
     U->ray_u = A.cam.camera_type == 0 ? o0 : d0;
   }
-  const mcpt_material *mats = S.mats;
+  typedef const __attribute__((address_space(3))) mcpt_material LdsMaterial;
+  LdsMaterial *const lds_mat_table = (LdsMaterial *)reinterpret_cast<mcpt_material *>(U + 1);
   if (A.lds_mats) {
     mcpt_material *lm = reinterpret_cast<mcpt_material *>(U + 1);
     for (int k = lane; k < S.n_mats; k += 64) lm[k] = S.mats[k];
-    mats = lm;
   }
   __syncthreads();
 
@@ -1217,7 +1217,11 @@ __global__ void __launch_bounds__(64, MCPT_WAVES_PER_SIMD) k_render(RenderArgs A
           in.pt = o + best_t * d;                                  // objdef.h:218
           in.mat = as_i(tn.w);
           bool rs = G && lst == kRes;
-          ShadeOut so = shade_hit<G>(mats, in, color, seed, A.max_depth, rs);
+          ShadeOut so;
+          if (A.lds_mats)  // LDS-typed reads (ds_read, no flat access waiting on vector memory)
+            so = shade_hit<G>(lds_mat_table, in, color, seed, A.max_depth, rs);
+          else
+            so = shade_hit<G>(S.mats, in, color, seed, A.max_depth, rs);
           pending = so.pending;
           lst = pending ? kRes : kBusy;
           if (!pending) {
