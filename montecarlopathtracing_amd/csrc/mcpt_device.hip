@@ -718,13 +718,21 @@ __device__ inline f4 accumulate_one(f4 now, f4 &hist, int32_t &cnt, int max_atte
 // that tag: the protocol needs each aligned 8-B granule untorn, nothing more
 // (no flag, no fence; MI355X_MICROARCH.md "handoff-1to1": data-tagged
 // granules are the cheapest hand-off).
+// The accesses are buffer loads / stores with the sc1 cache bit (aux 16:
+// write-through / coherent at agent scope) rather than volatile ones: volatile
+// made the compiler wait for each store to complete and each load to land
+// before the next memory instruction, a full memory round trip per 16 B.
 typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
-typedef __attribute__((address_space(1))) u64x2 g_u64x2;
-__device__ inline u64x2 handoff_load2(const unsigned long long *p) {
-  return *(const volatile g_u64x2 *)p;
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+__device__ inline __amdgpu_buffer_rsrc_t handoff_rsrc(unsigned long long *base) {
+  return __builtin_amdgcn_make_buffer_rsrc(base, 0, 0x7FFFFFFF, 0x00020000);
 }
-__device__ inline void handoff_store2(unsigned long long *p, unsigned long long a, unsigned long long b) {
-  *(volatile g_u64x2 *)p = (u64x2){a, b};
+__device__ inline u64x2 handoff_load2(__amdgpu_buffer_rsrc_t rs, uint32_t off) {
+  return __builtin_bit_cast(u64x2, __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 16));
+}
+__device__ inline void handoff_store2(__amdgpu_buffer_rsrc_t rs, uint32_t off, unsigned long long a,
+                                      unsigned long long b) {
+  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, (u64x2){a, b}), rs, off, 0, 16);
 }
 // This wave's XCD (0-7).  Picks the home queue: speed only — any placement
 // gives the same result, and waves steal from the other queues when theirs
@@ -1006,8 +1014,10 @@ __global__ void __launch_bounds__(64, MCPT_WAVES_PER_SIMD) k_render(RenderArgs A
           hist = A.hist[pp];
           cnt = A.count[pp];
         } else {  // published by another lane, any XCD
-          const unsigned long long *g = A.handoff + (size_t)pp * kHandoffWords;
-          const u64x2 h0 = handoff_load2(g), h1 = handoff_load2(g + 2);
+          const __amdgpu_buffer_rsrc_t hr = handoff_rsrc(A.handoff);
+          const uint32_t go = (uint32_t)pp * (uint32_t)(kHandoffWords * 8);
+          asm volatile("" ::: "memory");  // a poll: the granules are read again every iteration
+          const u64x2 h0 = handoff_load2(hr, go), h1 = handoff_load2(hr, go + 16);
           const unsigned long long want = (unsigned long long)(A.tag_base | (uint32_t)blk);
           ready = (h0.x >> 48) == want && (h0.y >> 48) == want && (h1.x >> 48) == want && (h1.y >> 48) == want;
           // 192 payload bits, 48 per granule: seed | mean.x | mean.y | mean.z | mean.w | count
@@ -1245,10 +1255,11 @@ __global__ void __launch_bounds__(64, MCPT_WAVES_PER_SIMD) k_render(RenderArgs A
               const unsigned long long tag = (unsigned long long)(A.tag_base | (uint32_t)(blk + 1)) << 48;
               const uint32_t w1 = (uint32_t)as_i(hist.x), w2 = (uint32_t)as_i(hist.y);
               const uint32_t w3 = (uint32_t)as_i(hist.z), w4 = (uint32_t)as_i(hist.w);
-              unsigned long long *g = A.handoff + (size_t)pid * kHandoffWords;
-              handoff_store2(g, tag | seed | (unsigned long long)(w1 & 0xFFFFu) << 32,
+              const __amdgpu_buffer_rsrc_t hr = handoff_rsrc(A.handoff);
+              const uint32_t go = (uint32_t)pid * (uint32_t)(kHandoffWords * 8);
+              handoff_store2(hr, go, tag | seed | (unsigned long long)(w1 & 0xFFFFu) << 32,
                              tag | (w1 >> 16) | (unsigned long long)w2 << 16);
-              handoff_store2(g + 2, tag | w3 | (unsigned long long)(w4 & 0xFFFFu) << 32,
+              handoff_store2(hr, go + 16, tag | w3 | (unsigned long long)(w4 & 0xFFFFu) << 32,
                              tag | (w4 >> 16) | (unsigned long long)(uint32_t)cnt << 16);
             } else {
               A.seeds[pid] = seed;
