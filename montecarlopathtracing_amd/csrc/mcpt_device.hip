@@ -724,8 +724,9 @@ __device__ inline f4 accumulate_one(f4 now, f4 &hist, int32_t &cnt, int max_atte
 // before the next memory instruction, a full memory round trip per 16 B.
 typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+constexpr uint32_t kHandoffMaxBytes = 0x7FFFFFFFu;  // images beyond it run without hand-offs (mcpt_render_frames)
 __device__ inline __amdgpu_buffer_rsrc_t handoff_rsrc(unsigned long long *base) {
-  return __builtin_amdgcn_make_buffer_rsrc(base, 0, 0x7FFFFFFF, 0x00020000);
+  return __builtin_amdgcn_make_buffer_rsrc(base, 0, (int)kHandoffMaxBytes, 0x00020000);
 }
 __device__ inline u64x2 handoff_load2(__amdgpu_buffer_rsrc_t rs, uint32_t off) {
   return __builtin_bit_cast(u64x2, __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 16));
@@ -2261,6 +2262,10 @@ int mcpt_render_frames(mcpt_ctx *ctx, const mcpt_scene *scene, const mcpt_camera
       fpl = std::max(fpl, (frames + 1) / 2);
     fpl = std::max(1, std::min({fpl, cap, frames}));
   }
+  // the hand-off area is addressed with 32-bit byte offsets below 2^31
+  // (handoff_rsrc): a larger image runs one block per pixel per launch (no
+  // hand-off; launches chain through the state arrays)
+  if ((int64_t)p->width * p->height * kHandoffWords * 8 > (int64_t)kHandoffMaxBytes) fpl = std::max(p->frames, 1);
   // blocks per launch: the hand-off tag holds 8 bits of block index, and
   // one launch covers at most ~4096 frames
   const int64_t max_blocks = std::max<int64_t>(

@@ -445,6 +445,31 @@ def test_frame_blocks_handoff_full_size(rnd):
     dsc.close()
 
 
+def test_image_beyond_handoff_range(rnd):
+    """The block hand-off addresses its per-pixel granules with 32-bit byte
+    offsets below 2^31 (67 M pixels); a larger image runs one block per pixel
+    per launch whatever frames_per_launch asks, so it completes, and with the
+    same bits as one explicit block."""
+    data, cam = scenes.cbox_diffuse(), S.parse_camera(scenes.CBOX_CAM)
+    w, h = 8192, 8200
+    assert w * h * 32 > 2 ** 31
+    dsc = rnd.upload(data)
+    seeds = R.default_seeds(w * h)
+    outs = []
+    try:
+        for fpl in (1, 3):
+            st = rnd.new_state(w, h, seeds)
+            rnd.render_frames(dsc, cam, st, 2, 1 << 20, 3, frames_per_launch=fpl)
+            torch.cuda.synchronize()
+            outs.append(st)
+        assert torch.equal(outs[0].hist, outs[1].hist) and torch.equal(outs[0].count, outs[1].count)
+        assert torch.equal(outs[0].seeds, outs[1].seeds)
+        assert int((outs[0].count > 0).sum()) > w * h // 100  # depth 2: 1.7 % of the paths reach the light
+    finally:
+        del outs
+        dsc.close()
+
+
 @needs_ref
 @pytest.mark.parametrize("name,getter,camjson,depth", [("cbox", scenes.cbox, scenes.CBOX_CAM, 8),
                                                        ("dining", scenes.dining, scenes.DINING_CAM, 16)])
