@@ -253,6 +253,9 @@ def main():
                     help="k_render fetch threshold (mcpt_tuning.fetch_threshold); 0: tuned like the S threshold")
     ap.add_argument("--block-entries", type=int, default=0,
                     help="k_render block sizing (mcpt_tuning.block_entries); 0: tuned like the S threshold")
+    ap.add_argument("--last-block-frames", type=int, default=0,
+                    help="k_render last block length (mcpt_tuning.last_block_frames, -1 equal blocks); "
+                         "0: tuned like the S threshold")
     args = ap.parse_args()
     global W, H_PER_GPU, DEPTH
     wl = WORKLOADS[args.workload]
@@ -295,6 +298,8 @@ def main():
         rnd.set_tuning(**dict(rnd.get_tuning(), fetch_threshold=args.fetch_threshold))
     if args.block_entries > 0:
         rnd.set_tuning(**dict(rnd.get_tuning(), block_entries=args.block_entries))
+    if args.last_block_frames != 0:
+        rnd.set_tuning(**dict(rnd.get_tuning(), last_block_frames=args.last_block_frames))
     shade_th = rnd.get_tuning()["shade_threshold"] or 32
     if args.schedule == "auto" and args.shade_threshold > 0:
         rnd.tune_schedule(dsc, cam, st, DEPTH, attempt, frames=max(1, min(args.steps, 64)), trials=3, **kw)
@@ -434,7 +439,9 @@ def main():
                           "shade_threshold": shade_th,
                           "fetch_threshold": rnd.get_tuning()["fetch_threshold"] or 1,
                           "block_entries": rnd.get_tuning()["block_entries"] or 8,
-                          "frames_per_block": fpb, "search_tree_nodes": search_tree},
+                          "frames_per_block": fpb,
+                          "last_block_frames": rnd.get_tuning()["last_block_frames"],
+                          "search_tree_nodes": search_tree},
                "active_Msegments_per_s": round(segments * n / elapsed / 1e6, 2),
                "scene_build_gpu_s": None if build_s is None else round(build_s, 3),
                "traced_Msegments_per_s": round(traced * n / elapsed / 1e6, 2),

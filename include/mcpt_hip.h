@@ -208,6 +208,13 @@ typedef struct mcpt_tuning {
                                the previous call's view, computes it; every
                                call with a matching one reads it), 1 always,
                                2 never                                          */
+  int32_t last_block_frames; /* auto frames-per-block, one-launch calls of two
+                               or more blocks: the last block of every pixel
+                               is this many frames and the others share the
+                               rest evenly (a short last block shortens the
+                               launch's tail); 0 auto (ceil(frames / 8) once
+                               there are >= 6 pixels per resident lane, else
+                               equal blocks), -1 equal blocks                 */
 } mcpt_tuning;
 
 /* ------------------------------------------------------- version / errors */

@@ -77,7 +77,7 @@ class App:
             # either way).  Not the block sizing: a long call runs max_block_frames-frame blocks whatever
             # block_entries says, so short trials of it would tune a regime the run never enters.
             self.renderer.tune(self.scene, self.camera, self.state, self.cfg.MAXDEPTH(), att, frames=16,
-                               block_entries=None, frames_per_launch=16)
+                               block_entries=None, last_block=False, frames_per_launch=16)
             self._tuned = True
         while todo > 0:
             n = todo if self.attempt_count > att else min(todo, att + 1 - self.attempt_count)

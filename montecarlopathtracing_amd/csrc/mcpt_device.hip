@@ -761,6 +761,7 @@ struct RenderArgs {
   int32_t stripe_rows, stripe_index, stripe_count;
   int32_t max_depth, max_attempt, frame_begin, frames;  // frames: of this launch
   int32_t fpl, blocks;         // frames per block, blocks in this launch
+  int32_t nb_head, fpl_tail;   // blocks >= nb_head have fpl_tail frames (nb_head = blocks: all fpl)
   unsigned long long *handoff; // per pixel: kHandoffWords tagged granules
   uint32_t tag_base;           // this launch's tag; a granule for block b carries tag_base | b (16 bits)
   int32_t stack_depth;
@@ -1245,10 +1246,11 @@ __global__ void __launch_bounds__(64, MCPT_WAVES_PER_SIMD) k_render(RenderArgs A
         }
         if (done) {
           // ColorOut: history runs while attemptCount <= MAX_ATTEMPT (colorout.cpp:56)
-          const int32_t f0 = blk * A.fpl;
+          const bool head = blk < A.nb_head;
+          const int32_t f0 = head ? blk * A.fpl : A.nb_head * A.fpl + (blk - A.nb_head) * A.fpl_tail;
           if (A.frame_begin + f0 + f <= A.max_attempt) (void)accumulate_one(color, hist, cnt, A.max_attempt);
           ++f;
-          const int32_t fend = min(A.fpl, A.frames - f0);
+          const int32_t fend = min(head ? A.fpl : A.fpl_tail, A.frames - f0);
           fresh = f < fend;
           if (f == fend) {  // block complete: write back, fetch another next iteration
             const int32_t pid = (int32_t)(pxy >> 16) * A.W + (int32_t)(pxy & 0xFFFFu);
@@ -1655,7 +1657,8 @@ int mcpt_set_tuning(mcpt_ctx *c, const mcpt_tuning *t) {
   if (!c) return mcpt::fail(MCPT_ERR_ARG, "set_tuning: null ctx");
   if (t && (t->stack_window < 0 || t->stack_window > 2 || t->quantized < 0 || t->quantized > 2 ||
             t->primary_cache < 0 || t->primary_cache > 2 || t->lds_pad < 0 || t->lds_pad > 65536 ||
-            t->queue_chunk > 4096 || t->leaf_threshold > 64 || t->shade_threshold > 64 || t->fetch_threshold > 64))
+            t->queue_chunk > 4096 || t->leaf_threshold > 64 || t->shade_threshold > 64 || t->fetch_threshold > 64 ||
+            t->last_block_frames < -1))
     return mcpt::fail(MCPT_ERR_ARG, "set_tuning: value out of range");
   if (t)
     c->tune = *t;
@@ -2241,6 +2244,8 @@ int mcpt_render_frames(mcpt_ctx *ctx, const mcpt_scene *scene, const mcpt_camera
   // 4 and 8 ranks, tools/sweep.py --stripes).
   const uint32_t n_items = (uint32_t)A.tiles_x * (uint32_t)((A.local_rows + 7) / 8) * 64u;
   int fpl = p->frames_per_launch;
+  bool tail_ok = false;  // auto plan with several entries per lane: a short last block may apply
+  double slots_per_px = 0;  // pixels per resident lane
   if (fpl <= 0) {
     const int frames = std::max(p->frames, 1);
     const double per_block = (double)n_items / (double)(grid * 64);  // entries per lane per block
@@ -2256,10 +2261,13 @@ int mcpt_render_frames(mcpt_ctx *ctx, const mcpt_scene *scene, const mcpt_camera
     // 1-12 % faster than 4-frame blocks; the C5 8-rank share, 2 pixels per
     // lane: 4 % faster than 5-frame blocks; tools/sweep.py --stripes --fpl)
     const double per_slot = (double)n_items / ((double)std::max(per_cu, 1) * ctx->n_cu * 64);  // vs resident lanes
+    slots_per_px = per_slot;
     if (per_slot < 0.75)
       fpl = frames;
     else if (per_slot <= 2.5)
       fpl = std::max(fpl, (frames + 1) / 2);
+    else
+      tail_ok = true;
     fpl = std::max(1, std::min({fpl, cap, frames}));
   }
   // the hand-off area is addressed with 32-bit byte offsets below 2^31
@@ -2273,6 +2281,32 @@ int mcpt_render_frames(mcpt_ctx *ctx, const mcpt_scene *scene, const mcpt_camera
                             (int64_t)kMaxBlocksPerLaunch}));
   const int64_t n_blocks_all = (p->frames + fpl - 1) / fpl;
   const int n_launch = (int)((n_blocks_all + max_blocks - 1) / max_blocks);
+  // a short last block (last_block_frames, auto plans of one launch with
+  // several entries per lane): the first nb-1 blocks share frames - L evenly
+  // and the last takes the remainder (<= L).  Entries are block-major, so the
+  // last block's entries are the launch's tail; shorter ones leave lanes idle
+  // for less time at its end.  Same blocks, same hand-offs, same bits.
+  // Auto: ceil(frames / 8) frames once a lane has at least 6 pixels (20-frame
+  // C3 -2 %, 16-frame C4 -2 %, 8-frame C5 -3 %); with fewer, the long head
+  // blocks' own chains end late (C2, 4 pixels per lane: +2-5 %), so auto
+  // leaves equal blocks there and Renderer.tune tries both.
+  int fpl_head = fpl;
+  A.nb_head = INT32_MAX;  // every block fpl frames
+  A.fpl_tail = fpl;
+  const bool tail_auto = T.last_block_frames == 0 && slots_per_px >= 6.0;
+  if (tail_ok && n_launch == 1 && n_blocks_all >= 2 && (T.last_block_frames > 0 || tail_auto)) {
+    const int nb = (int)n_blocks_all;
+    const int L = T.last_block_frames > 0 ? T.last_block_frames : (p->frames + 7) / 8;
+    if (L < fpl) {
+      const int head = (p->frames - L + nb - 2) / (nb - 1);
+      const int last = p->frames - (nb - 1) * head;
+      if (last >= 1 && last <= L) {
+        fpl_head = head;
+        A.nb_head = nb - 1;
+        A.fpl_tail = last;
+      }
+    }
+  }
   if (n_launch + 1 > ctx->queue_cap) {  // kQueues heads per launch (+ the primary pass), zeroed by memsets
     if (ctx->d_queue) HIP_OK(hipFree(ctx->d_queue));
     ctx->d_queue = nullptr;
@@ -2291,7 +2325,7 @@ int mcpt_render_frames(mcpt_ctx *ctx, const mcpt_scene *scene, const mcpt_camera
     HIP_OK(hipMemsetAsync(ctx->d_handoff, 0, bytes, st));  // tag 0 never matches (blocks >= 1)
     ctx->handoff_cap = n_px;
   }
-  A.fpl = fpl;
+  A.fpl = fpl_head;
   A.handoff = ctx->d_handoff;
   A.spill = ctx->d_spill;
   if (ctx->stats_on || kDebug || kTiming)
@@ -2348,6 +2382,8 @@ int mcpt_render_frames(mcpt_ctx *ctx, const mcpt_scene *scene, const mcpt_camera
           Ap.frames = 1;
           Ap.fpl = 1;
           Ap.blocks = 1;
+          Ap.nb_head = INT32_MAX;
+          Ap.fpl_tail = 1;
           Ap.prim = nullptr;
           Ap.prim_out = ctx->d_prim;
           Ap.queue = ctx->d_queue + (size_t)n_launch * kQueues * kQueueStride;
@@ -2406,7 +2442,7 @@ int mcpt_render_frames(mcpt_ctx *ctx, const mcpt_scene *scene, const mcpt_camera
   // asynchronous: mcpt_get_stats waits for ev1 and reads the time and counters
   std::memset(&ctx->last, 0, sizeof(ctx->last));
   ctx->last.launches = launches;
-  ctx->last.frames_per_block = fpl;
+  ctx->last.frames_per_block = fpl_head;
   ctx->last.stack_window = win ? 1 : 0;
   ctx->last.quantized = kind == 2 ? 1 : 0;
   ctx->last.workgroups = (int32_t)grid;

@@ -223,11 +223,13 @@ class Renderer:
         return sched, {k[0]: v for k, v in best.items()}
 
     def tune(self, scene, camera, state, max_depth, max_attempt, frames=64, trials=1, shade_thresholds=(32, 40, 48),
-             fetch_thresholds=(1, 8), block_entries=(8, 16), **kw):
+             fetch_thresholds=(1, 8), block_entries=(8, 16), last_block=True, **kw):
         """tune_schedule over the leaf-test schedule, the S-phase threshold
         (mcpt_tuning.shade_threshold) and then the fetch threshold
         (mcpt_tuning.fetch_threshold), then the block sizing
-        (mcpt_tuning.block_entries): their best values differ by scene
+        (mcpt_tuning.block_entries), then a short last block against equal
+        blocks (mcpt_tuning.last_block_frames -1 or ceil(frames / 8); the
+        auto rule's value is kept when it is as fast): their best values differ by scene
         (round 2, 3-frame blocks: veach_mis S 40, fetch 8; cbox S 32-40, fetch 8;
         the 10 M-triangle soup S 32, fetch 1).  Every combination gives the same bits.  The
         winner goes to scene.schedule and the renderer's tuning.  Returns
@@ -274,11 +276,28 @@ class Renderer:
                             if t != th:
                                 trial(sched, t, fe, be)
                     sched, th, fe, be = min(best, key=lambda k: (best[k], k))
+            lb = base["last_block_frames"]
+            if shade_thresholds and last_block:  # then a short last block against equal blocks
+                lbs = {-1, (int(frames) + 7) // 8}
+                key = (sched, th, fe, be)
+                lbest = {lb: best[key]}
+                for _ in range(int(trials)):
+                    for v in sorted(lbs - {lb}):
+                        self.set_tuning(**dict(base, shade_threshold=th, fetch_threshold=fe, block_entries=be,
+                                               last_block_frames=v))
+                        scratch.seeds, scratch.hist, scratch.count = (state.seeds.clone(), state.hist.clone(),
+                                                                      state.count.clone())
+                        self.render_frames(scene, camera, scratch, max_depth, max_attempt, frames,
+                                           frame_begin=state.frames_done, schedule=sched, **kw)
+                        ms = self.stats()["kernel_ms"]
+                        lbest[v] = min(lbest.get(v, ms), ms)
+                lb = min(lbest, key=lambda k: (lbest[k], k))
         finally:
             self.set_tuning(**base)
         scene.schedule = sched
         if shade_thresholds:
-            self.set_tuning(**dict(base, shade_threshold=th, fetch_threshold=fe, block_entries=be))
+            self.set_tuning(**dict(base, shade_threshold=th, fetch_threshold=fe, block_entries=be,
+                                   last_block_frames=lb))
         return sched, th, best
 
     # ------------------------------------------------ wavefront (drop-in)

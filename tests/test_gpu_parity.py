@@ -445,6 +445,37 @@ def test_frame_blocks_handoff_full_size(rnd):
     dsc.close()
 
 
+@pytest.mark.parametrize("diffuse", [True, False])
+def test_short_last_block_same_bits(rnd, diffuse):
+    """mcpt_tuning.last_block_frames: on an image with several pixels per
+    resident lane the auto plan's blocks become (long head blocks, one short
+    last block); the frame range each block covers and the MAX_ATTEMPT cut
+    inside the last block give the same bits as one block per pixel."""
+    data = scenes.cbox_diffuse() if diffuse else scenes.cbox()
+    cam = S.parse_camera(scenes.CBOX_CAM)
+    w = h = 1024
+    seeds = R.default_seeds(w * h)
+    dsc = rnd.upload(data)
+    try:
+        for attempt in (1 << 20, 18):
+            outs, fpbs = [], []
+            for t, fpl in (({}, 20), ({"last_block_frames": -1}, 0), ({"last_block_frames": 2}, 0),
+                           ({"last_block_frames": 3, "block_entries": 12}, 0), ({"last_block_frames": 9}, 0)):
+                rnd.set_tuning(**t)
+                st = rnd.new_state(w, h, seeds)
+                rnd.render_frames(dsc, cam, st, 8, attempt, 20, frames_per_launch=fpl)
+                torch.cuda.synchronize()
+                fpbs.append(rnd.stats()["frames_per_block"])
+                outs.append((st.hist.cpu().numpy(), st.count.cpu().numpy(), st.seeds_np()))
+            assert fpbs[0] == 20 and fpbs[2] == 18, fpbs  # (18, 2): the short last block did run
+            for o in outs[1:]:
+                for a, b, what in zip(outs[0], o, ("hist", "count", "seeds")):
+                    assert_bits_equal(a, b, what)
+    finally:
+        rnd.set_tuning()
+        dsc.close()
+
+
 def test_image_beyond_handoff_range(rnd):
     """The block hand-off addresses its per-pixel granules with 32-bit byte
     offsets below 2^31 (67 M pixels); a larger image runs one block per pixel
