@@ -76,8 +76,9 @@ def run(tag, args):
     cfg = json.loads(line.splitlines()[-1])["config"]
     quiet = bench + ["--no-cpu", "--no-cache-off", "--schedule", cfg["schedule"], "--shade-threshold", str(cfg.get("shade_threshold", 32)),
                      "--fetch-threshold", str(cfg.get("fetch_threshold", 1)),
-                     "--block-entries", str(cfg.get("block_entries", 8)),
-                     "--last-block-frames", str(cfg.get("last_block_frames", 0) or -1)]
+                     "--block-entries", str(cfg.get("block_entries", 8))]
+    if cfg.get("last_block_frames"):  # 0: the auto rule, which the pinned command keeps (it does not tune)
+        quiet += ["--last-block-frames", str(cfg["last_block_frames"])]
     sh(["rocprofv3", "--kernel-trace", "--stats", "--output-format", "csv", "-d", os.path.join(out, "trace"), "--"]
        + quiet, os.path.join(out, "trace.log"), 400)
     print("trace done", flush=True)
