@@ -572,6 +572,7 @@ def test_tune_schedule_leaves_state_alone(rnd):
         # the other two S thresholds again when the block sizing changed
         assert len(best2) in (8, 10) and int(st2.count.sum()) == 0
         assert (rnd.get_tuning()["block_entries"] or 8) in (8, 16)
+        assert rnd.get_tuning()["last_block_frames"] in (-1, 0, 1)  # equal, auto, or ceil(4 / 8)
         rnd.render_frames(dsc, cam, st2, 12, 1 << 20, 6)
         torch.cuda.synchronize()
         assert_bits_equal(st2.hist.cpu().numpy(), ref.hist.cpu().numpy(), "hist after tune")
@@ -682,6 +683,8 @@ def test_render_zero_frames_and_bad_params(rnd):
         rnd.render_frames(dsc, cam, st, 0, 4, 1)  # max_depth must be >= 1
     with pytest.raises(L.MCPTError):
         rnd.render_frames(dsc, cam, st, 4, 4, -1)
+    with pytest.raises(L.MCPTError):
+        rnd.set_tuning(last_block_frames=-2)  # -1 equal blocks, 0 auto, > 0 frames
     dsc.close()
 
 
