@@ -42,6 +42,27 @@ def test_abi_exports_every_declared_symbol():
     assert L.lib().mcpt_version().decode().startswith("mcpt-mi355x")
 
 
+def _header_fields(hdr, struct):
+    """int32 field names of `typedef struct <struct> {...}` in header order."""
+    body = re.search(r"typedef struct %s \{(.*?)\} %s;" % (struct, struct), hdr, re.S).group(1)
+    body = re.sub(r"/\*.*?\*/", "", body, flags=re.S)
+    names = []
+    for decl in body.split(";"):
+        m = re.match(r"\s*int32_t\s+(.*)", decl, re.S)
+        if m:
+            names += [n.strip() for n in m.group(1).split(",")]
+    return names
+
+
+def test_tuning_and_params_structs_match_header():
+    """mcpt_tuning grows at its end as knobs are added: the ctypes mirrors
+    (_lib.Tuning, _lib.RenderParams) must list the header's int32 fields in its
+    order, or Python would set the wrong knob."""
+    hdr = open(os.path.join(ROOT, "include", "mcpt_hip.h")).read()
+    assert [f for f, _ in L.Tuning._fields_] == _header_fields(hdr, "mcpt_tuning")
+    assert [f for f, _ in L.RenderParams._fields_] == _header_fields(hdr, "mcpt_render_params")
+
+
 def test_record_layouts_match_objdef():
     # objdef.h:21-99 sizes; the C structs are checked by the same numbers in the ABI tests below
     assert (L.CAMERA.itemsize, L.RAY.itemsize, L.HIT.itemsize) == (80, 48, 48)
