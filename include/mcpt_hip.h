@@ -123,7 +123,10 @@ typedef struct mcpt_render_params {
   int32_t mode;                     /* MCPT_MODE_*                          */
   int32_t frames_per_launch;        /* frames per block (a lane runs one pixel
                                        for one block, then hands it on);
-                                       <= 0: auto (mcpt_tuning.block_entries) */
+                                       <= 0: auto (mcpt_tuning.block_entries);
+                                       images over 67 M pixels (no hand-off
+                                       area) run one block of at most
+                                       max_block_frames frames per launch */
   int32_t schedule;                 /* MCPT_SCHED_*: how k_render batches leaf
                                        tests (results identical; speed only) */
 } mcpt_render_params;
@@ -189,7 +192,8 @@ typedef struct mcpt_tuning {
   int32_t block_entries;    /* auto frames-per-block: smallest block count (at
                                least 2) that gives every resident lane this many
                                queue entries (8)                                 */
-  int32_t max_block_frames; /* auto frames-per-block upper bound (32)            */
+  int32_t max_block_frames; /* frames-per-block upper bound of auto plans and of
+                               images over 67 M pixels (32)                      */
   int32_t stack_window;     /* 0 auto (default), 1 the 32-entry LDS window with
                                a global spill, 2 the whole stack in LDS          */
   int32_t lds_pad;          /* extra LDS bytes per workgroup (occupancy

@@ -50,17 +50,25 @@ def _main_dist(a):
     from . import dist as D
     from . import render as R
     from . import scene as S
+    from .app import config_scene
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # MCPT_DIST_SHARED_GPU=1 rehearses the N-rank job on a one-GPU box: every
+    # rank on device 0, gloo for the one reduce (tests/test_gpu_dist.py)
+    shared = os.environ.get("MCPT_DIST_SHARED_GPU") == "1"
+    if shared:
+        local = 0
     torch.cuda.set_device(local)
-    dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    if shared:
+        dist.init_process_group("gloo")
+    else:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     cfg = C.Config(a.config, a.configid)
+    if not cfg.USEOPENCL():
+        raise ValueError('config has "opencl": false — the reference throws "Not Implemented" here')
     root = os.path.dirname(os.path.abspath(a.config))
-    over = S.diffuse_only if cfg.entry.get("materials") == "diffuse_only" else None
-    data = S.SceneData.from_obj(os.path.join(root, cfg.GETDIRECTORY()), cfg.GETOBJNAME(), over)
-    if cfg.BVHTYPE() in ("treelet", "treeletGPU"):
-        data = data.with_nodes(R.treelet_device(data.nodes, local))
-    elif cfg.BVHTYPE() != "hlbvh":
-        raise ValueError("BVH Not Implemented: %r" % cfg.BVHTYPE())
+    # the same scene and tree as App.init: the GPU treelet pass over a fresh
+    # HLBVH for every bvhtype (scenebuild.cpp:66-95)
+    data = config_scene(cfg, root, local)
     rnd = R.Renderer(local)
     sc = rnd.upload(data)
     w, h = cfg.WIDTH(), cfg.HEIGHT()
@@ -69,7 +77,7 @@ def _main_dist(a):
                                frames, R.default_seeds(w * h))
     if dist.get_rank() == 0:
         path = os.path.join(a.out, cfg.GETOBJNAME() + ".hdr")
-        S.write_hdr(path, out[0].reshape(h, w, 4))
+        S.write_hdr(path, out[0].reshape(h, w, 4), flip=True)
         print("wrote", path)
     dist.destroy_process_group()
     return 0

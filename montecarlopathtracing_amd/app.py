@@ -16,6 +16,29 @@ from . import config as C
 from . import scene as S
 
 
+def config_scene(cfg, root, device=0, material_override=None):
+    """SceneCL's input for a config entry: the OBJ/MTL scene over the tree
+    every reference render traverses.  SceneCL's ctor (scenebuild.cpp:66-95):
+    whatever bvhtype names, the "hlbvh" and "treelet" branches fall through
+    into the GPUBVH block ("treeletGPU" jumps there), which uploads a FRESH
+    HLBVH over bvhBuffer and restructures it in place with the GPU treelet
+    kernel; intersect reads that buffer (:125).  "treelet"'s TreeletBVH<CPU>
+    tree (:70-73) is built and then overwritten, so it is not computed here.
+    App.init and the multi-GPU CLI (__main__._main_dist) both load through
+    this, so every GPU count renders over the same tree."""
+    from . import render as R
+    directory = os.path.join(root, cfg.GETDIRECTORY())
+    if not directory.endswith("/"):
+        directory += "/"
+    if material_override is None and cfg.entry.get("materials") == "diffuse_only":
+        material_override = S.diffuse_only
+    data = S.SceneData.from_obj(directory, cfg.GETOBJNAME(), material_override)
+    bvhtype = cfg.BVHTYPE()
+    if bvhtype not in ("hlbvh", "treelet", "treeletGPU"):
+        raise ValueError("BVH Not Implemented: %r" % bvhtype)  # scenebuild.cpp:77-79
+    return data.with_nodes(R.treelet_gpu_device(data.nodes, device))
+
+
 class App:
     def __init__(self, cfg, configid=None, device=0, seeds=None, out_dir=".", root=None,
                  material_override=None):
@@ -45,20 +68,7 @@ class App:
             # (raygeneration.cpp:51-56 vs OpenCLApp.cpp:38-51); a mismatch is undefined there
             raise ValueError("camera.resolution must equal width/height")
         self.w, self.h = self.cfg.WIDTH(), self.cfg.HEIGHT()
-        directory = os.path.join(self.root, self.cfg.GETDIRECTORY())
-        if not directory.endswith("/"):
-            directory += "/"
-        self.data = S.SceneData.from_obj(directory, self.cfg.GETOBJNAME(), self.material_override)
-        # SceneCL ctor (scenebuild.cpp:66-95): whatever bvhtype names, the
-        # "hlbvh" and "treelet" branches fall through into the GPUBVH block
-        # ("treeletGPU" jumps there), which uploads a FRESH HLBVH over bvhBuffer
-        # and restructures it in place with the GPU treelet kernel; intersect
-        # reads that buffer (:125).  "treelet"'s TreeletBVH<CPU> tree (:70-73)
-        # is built and then overwritten, so it is not computed here.
-        bvhtype = self.cfg.BVHTYPE()
-        if bvhtype not in ("hlbvh", "treelet", "treeletGPU"):
-            raise ValueError("BVH Not Implemented: %r" % bvhtype)  # scenebuild.cpp:77-79
-        self.data = self.data.with_nodes(R.treelet_gpu_device(self.data.nodes, self.device))
+        self.data = config_scene(self.cfg, self.root, self.device, self.material_override)
         self.camera = S.parse_camera(cam)
         self.renderer = R.Renderer(self.device)
         self.scene = self.renderer.upload(self.data)

@@ -2243,6 +2243,7 @@ int mcpt_render_frames(mcpt_ctx *ctx, const mcpt_scene *scene, const mcpt_camera
   // blocks there keep at least 4 frames (measured on C2 and C4 shares of 2,
   // 4 and 8 ranks, tools/sweep.py --stripes).
   const uint32_t n_items = (uint32_t)A.tiles_x * (uint32_t)((A.local_rows + 7) / 8) * 64u;
+  const int cap = T.max_block_frames > 0 ? T.max_block_frames : 32;  // frames per block at most (auto plans)
   int fpl = p->frames_per_launch;
   bool tail_ok = false;  // auto plan with several entries per lane: a short last block may apply
   double slots_per_px = 0;  // pixels per resident lane
@@ -2250,7 +2251,6 @@ int mcpt_render_frames(mcpt_ctx *ctx, const mcpt_scene *scene, const mcpt_camera
     const int frames = std::max(p->frames, 1);
     const double per_block = (double)n_items / (double)(grid * 64);  // entries per lane per block
     const int want = T.block_entries > 0 ? T.block_entries : kDefaultBlockEntries;
-    const int cap = T.max_block_frames > 0 ? T.max_block_frames : 32;
     int nb = std::max(2, (int)std::ceil(want / std::max(per_block, 1e-9)));
     nb = std::max(1, std::min(nb, frames));
     fpl = (frames + nb - 1) / nb;
@@ -2271,12 +2271,14 @@ int mcpt_render_frames(mcpt_ctx *ctx, const mcpt_scene *scene, const mcpt_camera
     fpl = std::max(1, std::min({fpl, cap, frames}));
   }
   // the hand-off area is addressed with 32-bit byte offsets below 2^31
-  // (handoff_rsrc): a larger image runs one block per pixel per launch (no
-  // hand-off; launches chain through the state arrays)
-  if ((int64_t)p->width * p->height * kHandoffWords * 8 > (int64_t)kHandoffMaxBytes) fpl = std::max(p->frames, 1);
+  // (handoff_rsrc): a larger image runs ONE block per launch, at most `cap`
+  // frames (no hand-off; launches chain through the state arrays, so every
+  // launch stays bounded: ~67 M+ pixels x 32 frames)
+  const bool no_handoff = (int64_t)p->width * p->height * kHandoffWords * 8 > (int64_t)kHandoffMaxBytes;
+  if (no_handoff) fpl = std::max(1, std::min(std::max(p->frames, 1), cap));
   // blocks per launch: the hand-off tag holds 8 bits of block index, and
   // one launch covers at most ~4096 frames
-  const int64_t max_blocks = std::max<int64_t>(
+  const int64_t max_blocks = no_handoff ? 1 : std::max<int64_t>(
       1, std::min<int64_t>({(int64_t)INT32_MAX / std::max<uint32_t>(n_items, 1), 4096 / fpl + 1,
                             (int64_t)kMaxBlocksPerLaunch}));
   const int64_t n_blocks_all = (p->frames + fpl - 1) / fpl;
@@ -2300,7 +2302,7 @@ int mcpt_render_frames(mcpt_ctx *ctx, const mcpt_scene *scene, const mcpt_camera
     if (L < fpl) {
       const int head = (p->frames - L + nb - 2) / (nb - 1);
       const int last = p->frames - (nb - 1) * head;
-      if (last >= 1 && last <= L) {
+      if (last >= 1 && last <= L && head <= cap) {  // the head blocks keep the block cap
         fpl_head = head;
         A.nb_head = nb - 1;
         A.fpl_tail = last;
@@ -2316,7 +2318,7 @@ int mcpt_render_frames(mcpt_ctx *ctx, const mcpt_scene *scene, const mcpt_camera
     ctx->queue_cap = cap;
   }
   const int64_t n_px = (int64_t)p->width * p->height;
-  if (n_blocks_all > 1 && n_px > ctx->handoff_cap) {
+  if (max_blocks > 1 && n_blocks_all > 1 && n_px > ctx->handoff_cap) {
     if (ctx->d_handoff) HIP_OK(hipFree(ctx->d_handoff));
     ctx->d_handoff = nullptr;
     ctx->handoff_cap = 0;

@@ -291,7 +291,8 @@ class Renderer:
                                            frame_begin=state.frames_done, schedule=sched, **kw)
                         ms = self.stats()["kernel_ms"]
                         lbest[v] = min(lbest.get(v, ms), ms)
-                lb = min(lbest, key=lambda k: (lbest[k], k))
+                # ties go to the baseline (the auto rule's value), then to the smaller key
+                lb = min(lbest, key=lambda k: (lbest[k], k != base["last_block_frames"], k))
         finally:
             self.set_tuning(**base)
         scene.schedule = sched

@@ -655,3 +655,81 @@ def test_png_preview_round_trip(tmp_path):
     want = np.floor(want * 255 + 0.5).astype(np.uint8)
     assert got.shape == (37, 53, 3) and np.array_equal(got, want)
     assert np.array_equal(got[-1, 0], [0, 255, 0])  # NaN -> 0, +inf -> 1, -inf -> 0 (bottom row, flipped)
+
+
+TREELET_CL = "/root/reference/MonteCarloPathTracing/kernels/treeletBVH.cl"
+
+
+def _cl_table(text, name):
+    """The integer initialiser of `__constant const <type> name[...] = {...};`
+    in treeletBVH.cl, as nested lists (comments stripped)."""
+    import re
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    text = re.sub(r"//[^\n]*", "", text)
+    m = re.search(r"\b%s\s*(\[[^\]]*\])+\s*=\s*(\{.*?\})\s*;" % re.escape(name), text, flags=re.S)
+    assert m, name
+    body = m.group(2)
+    rows = re.findall(r"\{([^{}]*)\}", body[1:-1]) if body.count("{") > 1 else [body[1:-1]]
+    return [[int(x) for x in r.replace("\n", " ").split(",") if x.strip()] for r in rows]
+
+
+@pytest.mark.skipif(not os.path.exists(TREELET_CL), reason="the reference is only in the build container")
+def test_treelet_cl_dp_schedule_tables():
+    """The DP round tables of the reference's GPU treelet kernel
+    (kernels/treeletBVH.cl:193-228), read from the reference itself, hold
+    what the restatement (csrc/mcpt_treelet_gpu.hip, oracle/
+    mcpt_oracle_treelet_gpu.cpp) assumes of them:
+    - roundConstant's five rounds list every 2..5-leaf mask of the 7-leaf
+      treelet exactly once, constLen rows long, and every mask comes after
+      all of its 2+-leaf subsets (so any order of each mask after its
+      subsets computes the same DP);
+    - roundSixConstant lists the seven 6-leaf masks; roundSixPart[i] is the
+      increasing list of the non-empty subsets of that mask without its
+      lowest bit (31 partitions, one per lane);
+    - roundSeven lists the 63 even masks 2..126 and leaves entry 63 zero:
+      lane 31's second candidate reads copt[0] (assumption A2)."""
+    text = open(TREELET_CL).read()
+    rc = _cl_table(text, "roundConstant")
+    cl = _cl_table(text, "constLen")[0]
+    assert [len(r) for r in rc] == cl == [10, 20, 29, 32, 21]
+    flat = [m for r in rc for m in r]
+    want = sorted(m for m in range(1, 127) if 2 <= bin(m).count("1") <= 5)
+    assert sorted(flat) == want and len(flat) == len(set(flat)) == 112
+    round_of = {m: k for k, r in enumerate(rc) for m in r}
+    for m in flat:  # every 2+-leaf proper subset is in a strictly earlier round
+        s = (m - 1) & m
+        while s:
+            if bin(s).count("1") >= 2:
+                assert round_of[s] < round_of[m], (s, m)
+            s = (s - 1) & m
+    six = _cl_table(text, "roundSixConstant")[0]
+    assert six == sorted(m for m in range(127) if bin(m).count("1") == 6) == [63, 95, 111, 119, 123, 125, 126]
+    parts = _cl_table(text, "roundSixPart")
+    assert len(parts) == 7
+    for m, p in zip(six, parts):
+        rest = m & ~(m & -m)  # the mask without its lowest bit
+        subs = sorted(s for s in range(1, 128) if s & ~rest == 0)
+        assert p == subs and len(p) == 31, m
+    seven = _cl_table(text, "roundSeven")[0]
+    assert seven == list(range(2, 127, 2)) and len(seven) == 63  # 64-entry array: [63] is zero-initialised
+    import re
+    assert re.search(r"roundSeven\s*\[\s*64\s*\]", text)
+
+
+def test_integration_snippet_matches_abi_host():
+    """INTEGRATION.md's "binding a maintainer would add" makes the C ABI calls
+    of the tested binding (tests/native/abi_host.cpp: init, then update up
+    to the .hdr dump), in the same order -- the GPU treelet pass over the
+    HLBVH included (scenebuild.cpp:87-95; VERDICT r3 weak 1: the snippet
+    used to skip it)."""
+    import re
+    doc = open(os.path.join(ROOT, "INTEGRATION.md")).read()
+    sec = doc.split("## The binding a maintainer would add", 1)[1]
+    snippet = sec.split("```cpp", 1)[1].split("```", 1)[0]
+    src = open(os.path.join(ROOT, "tests", "native", "abi_host.cpp")).read()
+    body = src[src.index("OK(mcpt_ctx_create"):]
+    body = body[:body.index("OK(mcpt_write_hdr") + 1]
+    calls = lambda t: re.findall(r"OK\((mcpt_\w+)\(", t)  # noqa: E731
+    want = calls(body) + ["mcpt_write_hdr"]
+    assert calls(snippet) == want
+    assert "mcpt_treelet_gpu" in want

@@ -137,6 +137,24 @@ def test_gpu_treelet_gpu_on_device_built_hlbvh_1m():
     assert st[6] == 0
 
 
+def test_gpu_treelet_gpu_c5_10m():
+    """C5's own tree at full size: the 10 M-triangle
+    random mesh (seed 42, +2 light triangles) built as bench.py --workload C5
+    builds it -- the GPU HLBVH, then the GPU treelet pass, in HBM -- equals
+    the oracle's sequential treelet pass over the host HLBVH, node for node."""
+    tris = S.random_mesh(10_000_000, build=lambda t: None).tris
+    d = R.build_hlbvh_device(tris)
+    R.treelet_gpu_device(d)
+    mine = R.records(d, L.BVHNODE)
+    del d
+    host = S.build_hlbvh(tris)
+    ref, st = _treelet_gpu_ref(host)
+    del host
+    assert len(mine) == 2 * len(tris) - 1
+    assert_bits_equal(mine, ref, "C5 device pipeline")
+    assert st[6] == 0
+
+
 def test_gpu_treelet_gpu_rejects_non_hlbvh_layout():
     nodes = S.build_hlbvh(_case("rand64"))
     bad = nodes.copy()

