@@ -22,7 +22,12 @@ The timed call computes its own primary hits (k_primary, then k_render reads
 them at every frame start): nothing the warmup computed is reused.
 
 Also reported (rank 0; cpu_baseline at N=1 only):
-  roofline     — the hot kernel k_render against HBM.  traffic = memory-side
+  roofline     — the hot kernel k_render against the unit that binds it: "td"
+                 (the vector-memory data path: the launch's gather floor from
+                 its own counters x the microbenchmark's per-instruction and
+                 per-line costs, as a share of its cycles) on the cache-resident
+                 scenes, "hbm" where HBM's fraction is the larger; both are
+                 reported (roofline.td, roofline.hbm).  traffic = memory-side
                  bytes per launch (rocprofv3 FETCH_SIZE x the calibrated scale
                  + WRITE_SIZE, the timed launch of this same command, committed
                  in profiles/pmc_summary.json by tools/profile.py); achieved =
@@ -412,6 +417,33 @@ def main():
                       "gather_latency_cycles_per_vmem_rd", "fetch_scale_calibrated", "timed_launch_ms_rocprof"):
                 roof[k] = prof.get(k)
             roof["profile"] = prof.get("source")
+            # the unit that binds: the vector-memory data path (TD) on the
+            # cache-resident scenes.  Measured: the launch's TD
+            # busy cycles per CU (rocprofv3 TD_TD_BUSY of this command's timed
+            # launch) against the busy fraction of the microbenchmark that
+            # saturates TD with k_render's node-step shape (tools/mb/td_lanes.hip),
+            # so achieved = busy cycles per CU / launch time, peak = the shader
+            # clock x that saturated busy fraction, frac = the launch's share of
+            # what TD sustains.  The modelled floor (the launch's own gather
+            # instructions and line accesses at the microbenchmark's per-
+            # instruction and per-line costs) is beside it.  HBM stays beside
+            # both (roofline.hbm) and is the bound where its fraction is larger.
+            td = prof.get("td_model")
+            hbm = {"achieved": roof["achieved"], "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": roof["frac"],
+                   "traffic": traffic}
+            roof["hbm"] = hbm
+            clk = prof.get("clock_GHz")
+            if td and clk and td.get("busy_frac"):
+                sat = td["td_busy_saturated_microbench"]
+                roof["td"] = {"achieved": round(td["td_busy"] * clk, 4), "peak": round(sat * clk, 4),
+                              "unit": "G TD-busy cycles/s per CU", "frac": td["busy_frac"],
+                              "model_floor_frac": td["model_frac"],
+                              "a_cycles_per_gather_inst": td["a_cycles_per_inst"],
+                              "b_cycles_per_line": td["b_cycles_per_line"],
+                              "vmem_rd_insts": td["vmem_rd_insts"], "l1_line_accesses": td["l1_accesses"]}
+                if roof["td"]["frac"] > (hbm["frac"] or 0):
+                    roof.update({"bound": "td", "achieved": roof["td"]["achieved"], "peak": roof["td"]["peak"],
+                                 "unit": roof["td"]["unit"], "frac": roof["td"]["frac"]})
         ec = e_counts(args.workload)
         if ec:
             b_seg = 328.0 + 64.0 * (ec["E_node"] + ec["E_tri"])

@@ -368,6 +368,15 @@ int mcpt_gamma_preview(mcpt_ctx *ctx, const float *color_dev, float *out_dev, in
 int mcpt_set_stats(mcpt_ctx *ctx, int32_t enabled);
 int mcpt_get_stats(mcpt_ctx *ctx, mcpt_stats *out);
 
+/* Diagnostics (MCPT_PHASE_TIMING builds, libmcpt_hip_timing.so): the
+ * timeline of every workgroup of the last render call's last k_render
+ * launch, 4 words each: start, the first moment one of its lanes found every
+ * work queue dry, end (s_memrealtime ticks, 100 MHz, chip-wide clock), and
+ * (loop iterations << 32 | queue entries started).  Waits for the call.
+ * Release builds log nothing: *n_workgroups = 0.  out may be NULL to ask
+ * for the count.                                                           */
+int mcpt_get_wave_log(mcpt_ctx *ctx, uint64_t *out, int64_t cap_workgroups, int64_t *n_workgroups);
+
 /* HLBVH::build (MCPT/BVH/hlbvh.cpp:92-200) on the GPU: triangles and the
  * 2n-1 output nodes are DEVICE pointers; the tree is bit-identical to
  * mcpt_build_hlbvh's (finite vertices).  Synchronises `stream`.           */

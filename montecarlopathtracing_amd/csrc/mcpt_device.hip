@@ -243,6 +243,8 @@ struct mcpt_ctx {
   PrimKey prim_key;                       // what d_prim holds
   bool seen_valid = false;
   PrimKey seen_key;                       // the previous render call's view
+  unsigned long long *d_wave_log = nullptr;  // MCPT_PHASE_TIMING: 4 words per workgroup of the last launch
+  int64_t wave_log_cap = 0, wave_log_n = 0;
 };
 
 struct mcpt_state {
@@ -775,6 +777,7 @@ struct RenderArgs {
   int32_t spill_stride;       // entries per lane (stack depth - window)
   const PrimHit *prim;        // per-pixel primary hits (k_primary), nullptr: trace segment 0
   PrimHit *prim_out;          // PRIM launches: where each pixel's primary hit goes
+  unsigned long long *wave_log;  // MCPT_PHASE_TIMING: 4 words per workgroup (mcpt_get_wave_log), or nullptr
 };
 
 __device__ inline int32_t global_row(int32_t lr, const RenderArgs &A) {
@@ -943,6 +946,11 @@ __global__ void __launch_bounds__(64, MCPT_WAVES_PER_SIMD) k_render(RenderArgs A
 #ifdef MCPT_PHASE_TIMING
   uint64_t ph[4] = {0, 0, 0, 0};
   uint64_t tick = __builtin_amdgcn_s_memtime();
+  // the wave's timeline (mcpt_get_wave_log): start, the first iteration a
+  // lane found every queue dry, end (s_memrealtime, 100 MHz, chip-wide),
+  // entries started
+  const uint64_t rt_start = __builtin_amdgcn_s_memrealtime();
+  uint64_t rt_dry = 0, n_started = 0, w_it_log = 0;
 #endif
   for (;;) {
     // ---- fetch: lanes without work take the next queue entries, from the
@@ -1005,6 +1013,9 @@ __global__ void __launch_bounds__(64, MCPT_WAVES_PER_SIMD) k_render(RenderArgs A
           } else if (((qs >> 8) & 15u) >= nq) {
             lst = kDead;  // every queue is dry
           }
+#ifdef MCPT_PHASE_TIMING
+          if (lst == kDead && rt_dry == 0) rt_dry = __builtin_amdgcn_s_memrealtime();
+#endif
         }
       }
       if (lst == kPend) {  // start the entry once its pixel's previous block is published
@@ -1034,10 +1045,16 @@ __global__ void __launch_bounds__(64, MCPT_WAVES_PER_SIMD) k_render(RenderArgs A
           f = 0;
           begin_frame();
         }
+#ifdef MCPT_PHASE_TIMING
+        n_started += (uint64_t)__popcll(__ballot(ready));
+#endif
       }
     }
     MCPT_TICK(0);
     if (!__ballot(lst != kDead)) break;
+#ifdef MCPT_PHASE_TIMING
+    ++w_it_log;
+#endif
     const bool live = G ? lst <= kBusy : lst == kBusy;  // (kRes only with glossy materials)
     // phase thresholds scaled to the wave's live lanes: a wave with few pixels
     // (a launch's tail, a strong-scaled rank) does not wait for lane counts
@@ -1285,6 +1302,23 @@ __global__ void __launch_bounds__(64, MCPT_WAVES_PER_SIMD) k_render(RenderArgs A
 #ifdef MCPT_PHASE_TIMING
   if (lane == 0)
     for (int k = 0; k < 4; ++k) atomicAdd(&A.stats[kPhaseSlot + k], (unsigned long long)ph[k]);
+  {
+    // the earliest lane's dry time (lanes record it in their own registers)
+    uint64_t dry = rt_dry ? rt_dry : ~0ull;
+    for (int off = 32; off > 0; off >>= 1) {
+      const uint64_t o2 = ((uint64_t)(uint32_t)__shfl_xor((int)(uint32_t)(dry >> 32), off) << 32) |
+                          (uint32_t)__shfl_xor((int)(uint32_t)dry, off);
+      dry = o2 < dry ? o2 : dry;
+    }
+    const uint64_t rt_end = __builtin_amdgcn_s_memrealtime();
+    if (A.wave_log && lane == 0) {
+      unsigned long long *w = A.wave_log + (size_t)blockIdx.x * 4;
+      w[0] = rt_start;
+      w[1] = dry == ~0ull ? rt_end : dry;
+      w[2] = rt_end;
+      w[3] = (w_it_log << 32) | (n_started & 0xFFFFFFFFull);
+    }
+  }
 #endif
   if (STATS) {
     atomicAdd(&A.stats[0], n_seg);
@@ -1479,6 +1513,7 @@ int mcpt_ctx_destroy(mcpt_ctx *c) {
   if (c->d_handoff) (void)hipFree(c->d_handoff);
   if (c->d_spill) (void)hipFree(c->d_spill);
   if (c->d_prim) (void)hipFree(c->d_prim);
+  if (c->d_wave_log) (void)hipFree(c->d_wave_log);
   if (c->ev0) (void)hipEventDestroy(c->ev0);
   if (c->ev1) (void)hipEventDestroy(c->ev1);
   if (c->ev_prim) (void)hipEventDestroy(c->ev_prim);
@@ -1650,6 +1685,17 @@ int mcpt_get_stats(mcpt_ctx *c, mcpt_stats *out) {
     }
   }
   *out = c->last;
+  return MCPT_OK;
+}
+
+int mcpt_get_wave_log(mcpt_ctx *c, uint64_t *out, int64_t cap_workgroups, int64_t *n_workgroups) {
+  if (!c || !n_workgroups) return mcpt::fail(MCPT_ERR_ARG, "get_wave_log: null");
+  *n_workgroups = c->wave_log_n;
+  if (!out || c->wave_log_n == 0) return MCPT_OK;
+  if (cap_workgroups < c->wave_log_n) return mcpt::fail(MCPT_ERR_ARG, "get_wave_log: buffer too small");
+  HIP_OK(hipSetDevice(c->device));
+  if (c->last_pending) HIP_OK(hipEventSynchronize(c->ev1));
+  HIP_OK(hipMemcpy(out, c->d_wave_log, (size_t)c->wave_log_n * 4 * sizeof(uint64_t), hipMemcpyDeviceToHost));
   return MCPT_OK;
 }
 
@@ -2275,7 +2321,7 @@ int mcpt_render_frames(mcpt_ctx *ctx, const mcpt_scene *scene, const mcpt_camera
   // frames (no hand-off; launches chain through the state arrays, so every
   // launch stays bounded: ~67 M+ pixels x 32 frames)
   const bool no_handoff = (int64_t)p->width * p->height * kHandoffWords * 8 > (int64_t)kHandoffMaxBytes;
-  if (no_handoff) fpl = std::max(1, std::min(std::max(p->frames, 1), cap));
+  if (no_handoff) fpl = std::max(1, std::min(p->frames_per_launch > 0 ? p->frames_per_launch : std::max(p->frames, 1), cap));
   // blocks per launch: the hand-off tag holds 8 bits of block index, and
   // one launch covers at most ~4096 frames
   const int64_t max_blocks = no_handoff ? 1 : std::max<int64_t>(
@@ -2330,6 +2376,19 @@ int mcpt_render_frames(mcpt_ctx *ctx, const mcpt_scene *scene, const mcpt_camera
   A.fpl = fpl_head;
   A.handoff = ctx->d_handoff;
   A.spill = ctx->d_spill;
+  A.wave_log = nullptr;
+  ctx->wave_log_n = 0;
+  if (kTiming) {  // diagnostics: each launch's workgroups log their timeline (the last launch's remain)
+    if (grid > ctx->wave_log_cap) {
+      if (ctx->d_wave_log) HIP_OK(hipFree(ctx->d_wave_log));
+      ctx->d_wave_log = nullptr;
+      ctx->wave_log_cap = 0;
+      HIP_OK(hipMalloc(&ctx->d_wave_log, (size_t)grid * 4 * sizeof(unsigned long long)));
+      ctx->wave_log_cap = grid;
+    }
+    A.wave_log = ctx->d_wave_log;
+    ctx->wave_log_n = grid;
+  }
   if (ctx->stats_on || kDebug || kTiming)
     HIP_OK(hipMemsetAsync(ctx->d_stats, 0, kStatSlots * sizeof(unsigned long long), st));
   HIP_OK(hipEventRecord(ctx->ev0, st));
@@ -2388,6 +2447,7 @@ int mcpt_render_frames(mcpt_ctx *ctx, const mcpt_scene *scene, const mcpt_camera
           Ap.fpl_tail = 1;
           Ap.prim = nullptr;
           Ap.prim_out = ctx->d_prim;
+          Ap.wave_log = nullptr;
           Ap.queue = ctx->d_queue + (size_t)n_launch * kQueues * kQueueStride;
           HIP_OK(hipMemsetAsync(Ap.queue, 0, (size_t)kQueues * kQueueStride * sizeof(uint32_t), st));
           // its own resident grid: the PRIM form needs fewer registers

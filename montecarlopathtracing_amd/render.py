@@ -143,6 +143,22 @@ class Renderer:
         out["phase_ticks"] = list(out["phase_ticks"])
         return out
 
+    def wave_log(self):
+        """mcpt_get_wave_log (MCPT_PHASE_TIMING library only): per workgroup of
+        the last launch, (start, first-dry, end) in 100 MHz ticks and (iterations,
+        entries started) as an (n, 5) int64 array; empty on release builds."""
+        n = ctypes.c_int64()
+        L.check(L.lib().mcpt_get_wave_log(self.ctx, None, 0, ctypes.byref(n)))
+        if n.value == 0:
+            return np.zeros((0, 5), np.int64)
+        buf = np.zeros((n.value, 4), np.uint64)
+        L.check(L.lib().mcpt_get_wave_log(self.ctx, L.ptr(buf), n.value, ctypes.byref(n)))
+        out = np.zeros((n.value, 5), np.int64)
+        out[:, :3] = buf[:, :3].astype(np.int64)
+        out[:, 3] = (buf[:, 3] >> np.uint64(32)).astype(np.int64)
+        out[:, 4] = (buf[:, 3] & np.uint64(0xFFFFFFFF)).astype(np.int64)
+        return out
+
     def set_tuning(self, **knobs):
         """mcpt_set_tuning: k_render launch-plan knobs (leaf_threshold,
         shade_threshold, queue_chunk, block_entries, max_block_frames,

@@ -95,6 +95,15 @@ def run(tag, args):
         sh(["rocprofv3", "--pmc"] + PASSES[name] + ["--output-format", "csv", "-d", os.path.join(out, "calib_" + name),
                                                     "--"] + calib, os.path.join(out, "calib_%s.log" % name), 200)
     print("calibration done", flush=True)
+    # the TD model: cycles per gather instruction against the
+    # distinct lines it touches, by the committed microbenchmark, timed alone
+    # and then once under the counters the model multiplies (lines per
+    # instruction checked against TCP_TOTAL_CACHE_ACCESSES)
+    mb = os.path.join(ROOT, "tools", "mb", "td_lanes")
+    sh([mb, "--json"], os.path.join(out, "tdcal.jsonl"), 120)
+    sh(["rocprofv3", "--pmc", "SQ_INSTS_VMEM_RD", "TCP_TOTAL_CACHE_ACCESSES_sum", "TD_TD_BUSY_sum", "GRBM_GUI_ACTIVE",
+        "--output-format", "csv", "-d", os.path.join(out, "tdcal_pmc"), "--", mb], os.path.join(out, "tdcal_pmc.log"), 120)
+    print("TD calibration done", flush=True)
 
 
 def calib():
@@ -179,6 +188,7 @@ def summarize(tag):
     grbm = ctr["GRBM_GUI_ACTIVE"]  # summed over the 8 XCDs (MI355X_MICROARCH.md)
     cycles = grbm / 8.0
     l2_req = ctr["TCC_HIT_sum"] + ctr["TCC_MISS_sum"]
+    td = td_model(src, ctr, N_CU, cycles)
     summ = {
         "tag": tag, "command": "python3 bench.py " + " ".join(bench_args_of(bench)),
         "workload": bench["config"]["workload"], "steps": bench["steps"], "warmup": bench["warmup"],
@@ -224,6 +234,7 @@ def summarize(tag):
             "valu_busy": round(ctr["SQ_ACTIVE_INST_VALU"] / (N_CU * cycles), 4),
             "issue_frac": round(ctr["SQ_ACTIVE_INST_VALU"] / (N_CU * cycles) * ctr.get("VALUUtilization", float("nan")) / 100.0, 4),
             "td_busy": round(ctr.get("TD_TD_BUSY_sum", float("nan")) / (N_CU * cycles), 4)},
+        "td_model": td,
         "counters_timed_dispatch": ctr,
         "sources": ["profiles/%s_%s.csv" % (tag, x) for x in
                     ["kernel_stats", "kernel_trace"] + ["pmc_" + n for n in PASSES] + ["calib_fetch", "calib_write"]],
@@ -252,10 +263,68 @@ def summarize(tag):
                  "l2_hit_GBps_128B_lines": summ["l2_hit_GBps_128B_lines"],
                  "gather_latency_cycles_per_vmem_rd": summ["gather_latency_cycles_per_vmem_rd"],
                  "timed_launch_ms_rocprof": summ["timed_launch_ms_rocprof"], "frames_per_block": summ["frames_per_block"],
+                 "kernel_cycles": cycles, "clock_GHz": summ["clock_GHz"],
                  "source": "profiles/%s_summary.json" % tag}
+    if td:
+        allw[key]["td_model"] = {k: td[k] for k in ("a_cycles_per_inst", "b_cycles_per_line", "vmem_rd_insts",
+                                                    "l1_accesses", "floor_cycles_per_cu", "model_frac", "td_busy",
+                                                    "td_busy_saturated_microbench", "busy_frac")}
     with open(path, "w") as fh:
         json.dump(allw, fh, indent=1, sort_keys=True)
     print(json.dumps(summ, indent=1))
+
+
+def td_model(src, ctr, n_cu, cycles):
+    """The TD (vector-memory data path) bound of the timed launch, two ways.
+    Measured: TD_TD_BUSY per CU per cycle of the launch, against the same
+    counter on the microbenchmark's saturating pattern (tools/mb/td_lanes.hip
+    mode 0, 64 lanes each gathering their own 128-B record, 16 waves per CU:
+    k_render's node-step shape) -> busy_frac.  Modelled: the microbenchmark's
+    cycles per wave gather instruction per CU against the lines it touches,
+    fitted on its mode-0 points as cycles = a + b * lines; the launch's floor
+    is (a * SQ_INSTS_VMEM_RD + b * TCP_TOTAL_CACHE_ACCESSES) / CUs cycles and
+    model_frac = floor / kernel cycles.  None when the calibration was not
+    run (profiles before round 4)."""
+    path = os.path.join(src, "tdcal.jsonl")
+    if not os.path.exists(path):
+        return None
+    import numpy as np
+    tag = os.path.basename(src).replace("prof_", "")
+    pts = [json.loads(x) for x in open(path) if x.startswith("{")]
+    m0 = [p for p in pts if p["mode"] == 0]
+    A = np.array([[1.0, p["lines"]] for p in m0])
+    y = np.array([p["cycles_per_inst"] for p in m0])
+    (a, b), *_ = np.linalg.lstsq(A, y, rcond=None)
+    resid = y - A @ np.array([a, b])
+    shutil.copy(path, os.path.join(ROOT, "profiles", tag + "_tdcal.jsonl"))
+    # the counters' view of the same patterns (accesses per instruction = the
+    # designed lines; TD busy of the saturating pattern)
+    lines_ctr, sat = None, None
+    try:
+        f = newest(os.path.join(src, "tdcal_pmc", "*", "*_counter_collection.csv"))
+        shutil.copy(f, os.path.join(ROOT, "profiles", tag + "_tdcal_pmc.csv"))
+        ds = dispatches(f, r"^k\(|k\(float")
+        ids = sorted(ds)[1::2]  # each pattern: a warm dispatch, then the timed one
+        lines_ctr = [round(ds[i]["TCP_TOTAL_CACHE_ACCESSES_sum"] / max(ds[i]["SQ_INSTS_VMEM_RD"], 1), 2) for i in ids]
+        d0 = ds[ids[0]]  # mode 0, 64 active lanes
+        sat = d0["TD_TD_BUSY_sum"] / (n_cu * d0["GRBM_GUI_ACTIVE"] / 8.0)
+    except SystemExit:
+        pass
+    vm, acc = ctr["SQ_INSTS_VMEM_RD"], ctr["TCP_TOTAL_CACHE_ACCESSES_sum"]
+    floor = (a * vm + b * acc) / n_cu
+    busy = ctr["TD_TD_BUSY_sum"] / (n_cu * cycles)
+    return {"a_cycles_per_inst": round(float(a), 3), "b_cycles_per_line": round(float(b), 4),
+            "fit_max_abs_resid_cycles": round(float(np.abs(resid).max()), 2),
+            "points": [{k: p[k] for k in ("mode", "active", "lines", "cycles_per_inst")} for p in pts],
+            "counter_lines_per_inst": lines_ctr,
+            "vmem_rd_insts": vm, "l1_accesses": acc, "l1_accesses_per_vmem_rd": round(acc / max(vm, 1), 2),
+            "floor_cycles_per_cu": round(floor, 1), "kernel_cycles": cycles, "model_frac": round(floor / cycles, 4),
+            "td_busy": round(busy, 4), "td_busy_saturated_microbench": None if sat is None else round(sat, 4),
+            "busy_frac": None if not sat else round(busy / sat, 4),
+            "note": "busy_frac = the launch's TD busy / the saturating microbenchmark's (measured); model_frac = "
+                    "(a x SQ_INSTS_VMEM_RD + b x TCP_TOTAL_CACHE_ACCESSES_sum) / CUs / kernel cycles with a, b "
+                    "from the microbenchmark's own-line-per-lane points; a holds for any active-lane count (a "
+                    "1-lane gather costs ~18 cycles, a 64-lane one on 64 lines ~65), so SIMT efficiency moves it"}
 
 
 def bench_args_of(b):

@@ -1,0 +1,88 @@
+"""Where a short call's fixed cost goes (diagnostics): the
+timeline of every workgroup of one k_render launch, from the MCPT_PHASE_TIMING
+library's wave log (mcpt_get_wave_log: start, first dry queue, end; 100 MHz
+chip-wide ticks), for the bench's call shape.
+
+    MCPT_LIB_OVERRIDE=$PWD/montecarlopathtracing_amd/lib/libmcpt_hip_timing.so \\
+        python tools/tail_probe.py --workload C2 --frames 20 --fpl 0,5,10
+
+Per launch: span (first start to last end), the start spread, when the queues
+ran dry (first lane that found every queue empty) and how long workgroups
+kept running after it (the tail: percentiles of end - first dry), and the
+mean fraction of workgroups still running over that tail.
+"""
+import argparse
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402,F401
+
+import bench  # noqa: E402
+from montecarlopathtracing_amd import _lib as L  # noqa: E402
+from montecarlopathtracing_amd import render as R  # noqa: E402
+from montecarlopathtracing_amd import scene as S  # noqa: E402
+
+
+def summarize(log, ms):
+    st, dry, end = log[:, 0], log[:, 1], log[:, 2]
+    t0 = st.min()
+    us = lambda x: (x - t0) / 100.0  # noqa: E731 - 100 MHz ticks -> us
+    first_dry = dry.min()
+    tail = (end - first_dry) / 100.0
+    span = us(end.max())
+    # workgroups alive over the tail, sampled on 64 points
+    ts = np.linspace(first_dry, end.max(), 64)
+    alive = [(end > t).mean() for t in ts]
+    return {"kernel_ms": round(ms, 3), "span_us": round(float(span), 1),
+            "start_spread_us": round(float(us(st.max())), 1),
+            "first_dry_us": round(float(us(first_dry)), 1),
+            "tail_us_p50_p90_max": [round(float(np.percentile(tail, q)), 1) for q in (50, 90, 100)],
+            "tail_share_of_span": round(float((end.max() - first_dry) / 100.0 / span), 4),
+            "alive_mean_over_tail": round(float(np.mean(alive)), 4),
+            "iterations_p50_max": [int(np.percentile(log[:, 3], 50)), int(log[:, 3].max())],
+            "entries_per_wg_mean": round(float(log[:, 4].mean()), 2)}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--workload", default="C2", choices=sorted(bench.WORKLOADS))
+    ap.add_argument("--frames", type=int, default=20)
+    ap.add_argument("--fpl", default="0")
+    ap.add_argument("--tuning", default="shade_threshold=32,fetch_threshold=8,block_entries=16")
+    ap.add_argument("--out", default=os.path.join(ROOT, "gpurun_out", "tail_probe.jsonl"))
+    a = ap.parse_args()
+    wl = bench.WORKLOADS[a.workload]
+    data, camj = bench.load_scene(a.workload)
+    cam = S.parse_camera(camj)
+    rnd = R.Renderer(0)
+    dsc, _ = bench.upload_scene(rnd, data)
+    dsc.schedule = L.SCHED_PAIRED
+    if a.tuning:
+        rnd.set_tuning(**{k: int(v) for k, v in (x.split("=") for x in a.tuning.split(","))})
+    os.makedirs(os.path.dirname(a.out), exist_ok=True)
+    with open(a.out, "a") as fh:
+        for fpl in (int(x) for x in a.fpl.split(",")):
+            st = rnd.new_state(wl["w"], wl["h"])
+            rnd.render_frames(dsc, cam, st, wl["depth"], 1 << 30, 4, frames_per_launch=fpl)  # warm
+            for rep in range(3):
+                rnd.drop_caches()
+                rnd.render_frames(dsc, cam, st, wl["depth"], 1 << 30, a.frames, frames_per_launch=fpl)
+                s = rnd.stats()
+                log = rnd.wave_log()
+                if len(log) == 0:
+                    raise SystemExit("no wave log: run with the MCPT_PHASE_TIMING library (MCPT_LIB_OVERRIDE)")
+                rec = dict(workload=a.workload, frames=a.frames, fpl=fpl, frames_per_block=s["frames_per_block"],
+                           rep=rep, primary_ms=round(s.get("primary_ms", 0.0), 3), **summarize(log, s["kernel_ms"]))
+                print(json.dumps(rec), flush=True)
+                fh.write(json.dumps(rec) + "\n")
+    dsc.close()
+    rnd.close()
+
+
+if __name__ == "__main__":
+    main()
