@@ -368,6 +368,12 @@ int mcpt_gamma_preview(mcpt_ctx *ctx, const float *color_dev, float *out_dev, in
 int mcpt_set_stats(mcpt_ctx *ctx, int32_t enabled);
 int mcpt_get_stats(mcpt_ctx *ctx, mcpt_stats *out);
 
+/* Diagnostics: with stats on, every render call adds each pixel's segments
+ * (the chain of work its frames are, one sequential seed chain per pixel)
+ * into counts_dev[y * width + x] (width*height u32 on the device, zeroed by
+ * the caller); NULL stops it.                                              */
+int mcpt_set_pixel_segments(mcpt_ctx *ctx, uint32_t *counts_dev);
+
 /* Diagnostics (MCPT_PHASE_TIMING builds, libmcpt_hip_timing.so): the
  * timeline of every workgroup of the last render call's last k_render
  * launch, 4 words each: start, the first moment one of its lanes found every

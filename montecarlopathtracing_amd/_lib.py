@@ -107,6 +107,7 @@ SIGNATURES = {
     "mcpt_set_stats": (_I32, [_P, _I32]),
     "mcpt_get_stats": (_I32, [_P, _P]),
     "mcpt_get_wave_log": (_I32, [_P, _P, _I64, _P]),
+    "mcpt_set_pixel_segments": (_I32, [_P, _P]),
     "mcpt_selfcheck_trig": (_I32, [_P, _P, _P]),
     "mcpt_measure_read_bw": (_I32, [_P, _I64, _P]),
     "mcpt_gather_probe": (_I32, [_P, _I32, _I64, _P]),

@@ -217,6 +217,7 @@ struct mcpt_ctx {
   int device;
   int n_cu = 0;
   bool stats_on = false;
+  uint32_t *px_segments = nullptr;        // mcpt_set_pixel_segments (stats calls only)
   unsigned long long *d_stats = nullptr;  // segments, nodes, tris, bad, wave T/L/S phases
   uint32_t *d_queue = nullptr;            // k_render work-queue heads, kQueues per launch
   int32_t queue_cap = 0;                  // launches the head array holds
@@ -778,6 +779,7 @@ struct RenderArgs {
   const PrimHit *prim;        // per-pixel primary hits (k_primary), nullptr: trace segment 0
   PrimHit *prim_out;          // PRIM launches: where each pixel's primary hit goes
   unsigned long long *wave_log;  // MCPT_PHASE_TIMING: 4 words per workgroup (mcpt_get_wave_log), or nullptr
+  uint32_t *px_segments;      // STATS: each pixel's segments of the call added here (mcpt_set_pixel_segments), or nullptr
 };
 
 __device__ inline int32_t global_row(int32_t lr, const RenderArgs &A) {
@@ -860,6 +862,7 @@ __global__ void __launch_bounds__(64, MCPT_WAVES_PER_SIMD) k_render(RenderArgs A
   unsigned long long n_seg = 0, n_nodes = 0, n_tests = 0, n_bad = 0;
   unsigned long long w_t = 0, w_l = 0, w_s = 0, n_fb = 0;
   unsigned long long w_it = 0, n_wait = 0, n_idle = 0, n_rej = 0;
+  uint32_t px_seg = 0;  // STATS: segments of the lane's current entry (A.px_segments)
   // pixel state.  lst: this lane's role in the queue protocol, one small
   // int (one VGPR; kept out of lane-mask SGPR pairs on purpose, SGPRs are
   // the scarce register file of this kernel)
@@ -1231,7 +1234,7 @@ __global__ void __launch_bounds__(64, MCPT_WAVES_PER_SIMD) k_render(RenderArgs A
         A.prim_out[(size_t)(pxy >> 16) * (size_t)A.W + (pxy & 0xFFFFu)] = h;
         lst = kNeed;
       } else if (in_s) {
-        if (STATS && lst == kBusy) n_seg++;
+        if (STATS && lst == kBusy) n_seg++, px_seg++;
         bool done = false, fresh = false, pending = false;
         if (best_t >= kFltMax) {  // shade.cl:92-96 — miss: black, terminate
           color = (f4){0.0f, 0.0f, 0.0f, 0.0f};
@@ -1286,6 +1289,8 @@ __global__ void __launch_bounds__(64, MCPT_WAVES_PER_SIMD) k_render(RenderArgs A
               A.hist[pid] = hist;
               A.count[pid] = cnt;
             }
+            if (STATS && A.px_segments) atomicAdd(A.px_segments + pid, px_seg);
+            if (STATS) px_seg = 0;
             lst = kNeed;
           }
         }
@@ -1649,6 +1654,12 @@ int mcpt_gather_probe(mcpt_ctx *c, int32_t record_bytes, int64_t table_bytes, do
 int mcpt_set_stats(mcpt_ctx *c, int32_t on) {
   if (!c) return mcpt::fail(MCPT_ERR_ARG, "set_stats: null ctx");
   c->stats_on = on != 0;
+  return MCPT_OK;
+}
+
+int mcpt_set_pixel_segments(mcpt_ctx *c, uint32_t *counts_dev) {
+  if (!c) return mcpt::fail(MCPT_ERR_ARG, "set_pixel_segments: null ctx");
+  c->px_segments = counts_dev;
   return MCPT_OK;
 }
 
@@ -2377,6 +2388,7 @@ int mcpt_render_frames(mcpt_ctx *ctx, const mcpt_scene *scene, const mcpt_camera
   A.handoff = ctx->d_handoff;
   A.spill = ctx->d_spill;
   A.wave_log = nullptr;
+  A.px_segments = ctx->stats_on ? ctx->px_segments : nullptr;
   ctx->wave_log_n = 0;
   if (kTiming) {  // diagnostics: each launch's workgroups log their timeline (the last launch's remain)
     if (grid > ctx->wave_log_cap) {
@@ -2448,6 +2460,7 @@ int mcpt_render_frames(mcpt_ctx *ctx, const mcpt_scene *scene, const mcpt_camera
           Ap.prim = nullptr;
           Ap.prim_out = ctx->d_prim;
           Ap.wave_log = nullptr;
+          Ap.px_segments = nullptr;
           Ap.queue = ctx->d_queue + (size_t)n_launch * kQueues * kQueueStride;
           HIP_OK(hipMemsetAsync(Ap.queue, 0, (size_t)kQueues * kQueueStride * sizeof(uint32_t), st));
           // its own resident grid: the PRIM form needs fewer registers

@@ -143,6 +143,13 @@ class Renderer:
         out["phase_ticks"] = list(out["phase_ticks"])
         return out
 
+    def set_pixel_segments(self, counts):
+        """mcpt_set_pixel_segments: with stats on, render calls add each pixel's
+        segments into `counts` (an int32 CUDA tensor of width*height, zeroed by
+        the caller); None stops it."""
+        self._px_counts = counts  # kept alive while the library holds the pointer
+        L.check(L.lib().mcpt_set_pixel_segments(self.ctx, None if counts is None else L.ptr(counts)))
+
     def wave_log(self):
         """mcpt_get_wave_log (MCPT_PHASE_TIMING library only): per workgroup of
         the last launch, (start, first-dry, end) in 100 MHz ticks and (iterations,
