@@ -261,6 +261,9 @@ def main():
     ap.add_argument("--last-block-frames", type=int, default=0,
                     help="k_render last block length (mcpt_tuning.last_block_frames, -1 equal blocks); "
                          "0: tuned like the S threshold")
+    ap.add_argument("--tile-order", type=int, default=-1,
+                    help="k_render queue tile order (mcpt_tuning.tile_order: 0 dearest first by the costliest "
+                         "pixel, 1 image order, 2 by summed cost); -1: tuned with the block sizing")
     args = ap.parse_args()
     global W, H_PER_GPU, DEPTH
     wl = WORKLOADS[args.workload]
@@ -305,6 +308,8 @@ def main():
         rnd.set_tuning(**dict(rnd.get_tuning(), block_entries=args.block_entries))
     if args.last_block_frames != 0:
         rnd.set_tuning(**dict(rnd.get_tuning(), last_block_frames=args.last_block_frames))
+    if args.tile_order >= 0:
+        rnd.set_tuning(**dict(rnd.get_tuning(), tile_order=args.tile_order))
     shade_th = rnd.get_tuning()["shade_threshold"] or 32
     if args.schedule == "auto" and args.shade_threshold > 0:
         rnd.tune_schedule(dsc, cam, st, DEPTH, attempt, frames=max(1, min(args.steps, 64)), trials=3, **kw)
@@ -473,6 +478,8 @@ def main():
                           "block_entries": rnd.get_tuning()["block_entries"] or 8,
                           "frames_per_block": fpb,
                           "last_block_frames": rnd.get_tuning()["last_block_frames"],
+                          "tile_order": {0: "dearest first (costliest pixel)", 1: "image", 2: "dearest first (summed)"}[
+                              rnd.get_tuning()["tile_order"]],
                           "search_tree_nodes": search_tree},
                "active_Msegments_per_s": round(segments * n / elapsed / 1e6, 2),
                "scene_build_gpu_s": None if build_s is None else round(build_s, 3),

@@ -219,6 +219,12 @@ typedef struct mcpt_tuning {
                                launch's tail); 0 auto (ceil(frames / 8) once
                                there are >= 6 pixels per resident lane, else
                                equal blocks), -1 equal blocks                 */
+  int32_t tile_order;       /* order of the 8x8 pixel tiles in the work queues:
+                               0 auto (the primary-hit pass measures each
+                               pixel's primary-ray traversal; tiles whose
+                               costliest pixel is dearest start first, so the
+                               longest per-pixel chains do not start last), 1
+                               the image order, 2 by the tile's summed cost    */
 } mcpt_tuning;
 
 /* ------------------------------------------------------- version / errors */
@@ -370,18 +376,32 @@ int mcpt_get_stats(mcpt_ctx *ctx, mcpt_stats *out);
 
 /* Diagnostics: with stats on, every render call adds each pixel's segments
  * (the chain of work its frames are, one sequential seed chain per pixel)
- * into counts_dev[y * width + x] (width*height u32 on the device, zeroed by
- * the caller); NULL stops it.                                              */
-int mcpt_set_pixel_segments(mcpt_ctx *ctx, uint32_t *counts_dev);
+ * into counts_dev[y * width + x] and the k_render loop iterations its lane
+ * spent on it into iters_dev (width*height u32 each on the device, zeroed by
+ * the caller; either may be NULL); NULL, NULL stops it.                    */
+int mcpt_set_pixel_segments(mcpt_ctx *ctx, uint32_t *counts_dev, uint32_t *iters_dev);
+/* The primary-hit pass's per-pixel traversal cost of the cached view (loop
+ * iterations of k_render's PRIM form, or node steps + triangle tests of
+ * k_primary), width*height u32 to the host; *n = 0 when no cache is held. */
+int mcpt_get_primary_cost(mcpt_ctx *ctx, uint32_t *out, int64_t cap, int64_t *n);
 
 /* Diagnostics (MCPT_PHASE_TIMING builds, libmcpt_hip_timing.so): the
  * timeline of every workgroup of the last render call's last k_render
- * launch, 4 words each: start, the first moment one of its lanes found every
- * work queue dry, end (s_memrealtime ticks, 100 MHz, chip-wide clock), and
- * (loop iterations << 32 | queue entries started).  Waits for the call.
- * Release builds log nothing: *n_workgroups = 0.  out may be NULL to ask
- * for the count.                                                           */
+ * launch, 8 words each: start, the first moment one of its lanes found every
+ * work queue dry, end, the latest start of a queue entry (s_memrealtime
+ * ticks, 100 MHz, chip-wide clock), loop iterations, entries started,
+ * lane-iterations spent waiting for a pixel's previous block, XCD.  Waits
+ * for the call.  Release builds log nothing: *n_workgroups = 0.  out may be
+ * NULL to ask for the count.                                               */
 int mcpt_get_wave_log(mcpt_ctx *ctx, uint64_t *out, int64_t cap_workgroups, int64_t *n_workgroups);
+
+/* Diagnostics (MCPT_PHASE_TIMING builds): for a render call of one launch
+ * with at most 16 M (pixel, block) entries, the low 32 bits of the 100 MHz
+ * s_memrealtime clock at each entry's claim, start (its pixel's previous
+ * block published) and end, 3 words per entry at (pixel * blocks + block) * 3
+ * (0: never claimed).  *n_entries = pixels * blocks (0 otherwise, and on
+ * release builds).  Waits for the call.                                    */
+int mcpt_get_entry_log(mcpt_ctx *ctx, uint32_t *out, int64_t cap_entries, int64_t *n_entries, int32_t *blocks);
 
 /* HLBVH::build (MCPT/BVH/hlbvh.cpp:92-200) on the GPU: triangles and the
  * 2n-1 output nodes are DEVICE pointers; the tree is bit-identical to

@@ -57,7 +57,7 @@ class Tuning(ctypes.Structure):
     """mcpt_tuning: launch-plan knobs of k_render (speed only; 0 = default)."""
     _fields_ = [(n, ctypes.c_int32) for n in (
         "leaf_threshold", "shade_threshold", "queue_chunk", "block_entries", "max_block_frames", "stack_window",
-        "lds_pad", "queues", "fetch_threshold", "quantized", "primary_cache", "last_block_frames")]
+        "lds_pad", "queues", "fetch_threshold", "quantized", "primary_cache", "last_block_frames", "tile_order")]
 
 
 class MCPTError(RuntimeError):
@@ -107,7 +107,9 @@ SIGNATURES = {
     "mcpt_set_stats": (_I32, [_P, _I32]),
     "mcpt_get_stats": (_I32, [_P, _P]),
     "mcpt_get_wave_log": (_I32, [_P, _P, _I64, _P]),
-    "mcpt_set_pixel_segments": (_I32, [_P, _P]),
+    "mcpt_set_pixel_segments": (_I32, [_P, _P, _P]),
+    "mcpt_get_primary_cost": (_I32, [_P, _P, _I64, _P]),
+    "mcpt_get_entry_log": (_I32, [_P, _P, _I64, _P, _P]),
     "mcpt_selfcheck_trig": (_I32, [_P, _P, _P]),
     "mcpt_measure_read_bw": (_I32, [_P, _I64, _P]),
     "mcpt_gather_probe": (_I32, [_P, _I32, _I64, _P]),

@@ -158,7 +158,8 @@ constexpr int64_t kQuantAutoBytes = 32ll << 20;  // 8 XCDs x 4 MiB of L2
 // 1.66 (profiles/r02_primary_cache.txt)
 constexpr int64_t kPrimSmallTree = 1ll << 20;     // k_render counters (mcpt_stats)
 constexpr int kPhaseSlot = 16;     // MCPT_PHASE_TIMING: shader-clock ticks per phase (fetch, T, L, S)
-constexpr int kDebugSlot = 12;     // MCPT_DEBUG: violations of the stack bound, node and triangle indices
+constexpr int kDebugSlot = 12;
+constexpr int kWaveLogWords = 8;   // MCPT_PHASE_TIMING wave log (mcpt_get_wave_log)     // MCPT_DEBUG: violations of the stack bound, node and triangle indices
 
 // -DMCPT_DEBUG (make debug -> lib/libmcpt_hip_debug.so): k_render checks every
 // stack push against its capacity and every node / triangle index against
@@ -218,6 +219,7 @@ struct mcpt_ctx {
   int n_cu = 0;
   bool stats_on = false;
   uint32_t *px_segments = nullptr;        // mcpt_set_pixel_segments (stats calls only)
+  uint32_t *px_iters = nullptr;
   unsigned long long *d_stats = nullptr;  // segments, nodes, tris, bad, wave T/L/S phases
   uint32_t *d_queue = nullptr;            // k_render work-queue heads, kQueues per launch
   int32_t queue_cap = 0;                  // launches the head array holds
@@ -239,13 +241,21 @@ struct mcpt_ctx {
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   hipEvent_t ev_prim = nullptr;           // after k_primary, when the call ran it
   PrimHit *d_prim = nullptr;              // primary-hit cache, one record per pixel
+  uint32_t *d_prim_cost = nullptr;        // each cached pixel's primary-ray traversal cost (lane-iterations)
+  int32_t *d_tile_order = nullptr;        // queue position -> tile, dearest first (from d_prim_cost)
+  uint8_t *d_tile_key = nullptr;          // per tile: its cost, saturated to 8 bits
+  int64_t tile_cap = 0;
+  int32_t tile_order_mode = 0;            // the mcpt_tuning.tile_order value d_tile_order was built with (0: none)
   int64_t prim_cap = 0;                   // pixels
   bool prim_valid = false;
   PrimKey prim_key;                       // what d_prim holds
   bool seen_valid = false;
   PrimKey seen_key;                       // the previous render call's view
-  unsigned long long *d_wave_log = nullptr;  // MCPT_PHASE_TIMING: 4 words per workgroup of the last launch
+  unsigned long long *d_wave_log = nullptr;  // MCPT_PHASE_TIMING: kWaveLogWords per workgroup of the last launch
   int64_t wave_log_cap = 0, wave_log_n = 0;
+  uint32_t *d_entry_log = nullptr;        // MCPT_PHASE_TIMING: 3 words per (pixel, block) of the last launch
+  int64_t entry_log_cap = 0, entry_log_n = 0;
+  int32_t entry_log_blocks = 0;
 };
 
 struct mcpt_state {
@@ -780,6 +790,10 @@ struct RenderArgs {
   PrimHit *prim_out;          // PRIM launches: where each pixel's primary hit goes
   unsigned long long *wave_log;  // MCPT_PHASE_TIMING: 4 words per workgroup (mcpt_get_wave_log), or nullptr
   uint32_t *px_segments;      // STATS: each pixel's segments of the call added here (mcpt_set_pixel_segments), or nullptr
+  uint32_t *px_iters;         // STATS: each pixel's busy lane-iterations of the call, or nullptr
+  uint32_t *prim_cost;        // PRIM launches: each pixel's primary-ray lane-iterations (its traversal cost)
+  const int32_t *tile_order;  // queue position -> 8x8 tile (dearest first, mcpt_tuning.tile_order), or nullptr: image order
+  uint32_t *entry_log;        // MCPT_PHASE_TIMING: per (pixel, block) claim / start / end times (mcpt_get_entry_log), or nullptr
 };
 
 __device__ inline int32_t global_row(int32_t lr, const RenderArgs &A) {
@@ -862,7 +876,7 @@ __global__ void __launch_bounds__(64, MCPT_WAVES_PER_SIMD) k_render(RenderArgs A
   unsigned long long n_seg = 0, n_nodes = 0, n_tests = 0, n_bad = 0;
   unsigned long long w_t = 0, w_l = 0, w_s = 0, n_fb = 0;
   unsigned long long w_it = 0, n_wait = 0, n_idle = 0, n_rej = 0;
-  uint32_t px_seg = 0;  // STATS: segments of the lane's current entry (A.px_segments)
+  uint32_t px_seg = 0, px_it = 0;  // STATS: segments / busy iterations of the lane's current entry (A.px_*)
   // pixel state.  lst: this lane's role in the queue protocol, one small
   // int (one VGPR; kept out of lane-mask SGPR pairs on purpose, SGPRs are
   // the scarce register file of this kernel)
@@ -953,7 +967,7 @@ __global__ void __launch_bounds__(64, MCPT_WAVES_PER_SIMD) k_render(RenderArgs A
   // lane found every queue dry, end (s_memrealtime, 100 MHz, chip-wide),
   // entries started
   const uint64_t rt_start = __builtin_amdgcn_s_memrealtime();
-  uint64_t rt_dry = 0, n_started = 0, w_it_log = 0;
+  uint64_t rt_dry = 0, n_started = 0, w_it_log = 0, rt_last = 0, pend_it = 0;
 #endif
   for (;;) {
     // ---- fetch: lanes without work take the next queue entries, from the
@@ -1004,7 +1018,8 @@ __global__ void __launch_bounds__(64, MCPT_WAVES_PER_SIMD) k_render(RenderArgs A
           if (got) {
             const uint32_t items = queue_items(qx, n_tiles, nq);
             const uint32_t b = q / items, j = q - b * items;
-            const int32_t tile = (int32_t)((j >> 6) * nq + qx), k = (int32_t)(j & 63u);
+            const int32_t tpos = (int32_t)((j >> 6) * nq + qx), k = (int32_t)(j & 63u);
+            const int32_t tile = A.tile_order ? A.tile_order[tpos] : tpos;
             const int32_t x = (tile % A.tiles_x) * 8 + (k & 7);
             const int32_t lr = (tile / A.tiles_x) * 8 + (k >> 3);
             const int32_t y = lr < A.local_rows ? global_row(lr, A) : A.H;
@@ -1012,6 +1027,10 @@ __global__ void __launch_bounds__(64, MCPT_WAVES_PER_SIMD) k_render(RenderArgs A
               lst = kPend;
               blk = (int32_t)b;
               pxy = (uint32_t)x | ((uint32_t)y << 16);
+#ifdef MCPT_PHASE_TIMING
+              if (A.entry_log)
+                A.entry_log[((size_t)(y * A.W + x) * A.blocks + b) * 3] = (uint32_t)__builtin_amdgcn_s_memrealtime();
+#endif
             }
           } else if (((qs >> 8) & 15u) >= nq) {
             lst = kDead;  // every queue is dry
@@ -1049,7 +1068,12 @@ __global__ void __launch_bounds__(64, MCPT_WAVES_PER_SIMD) k_render(RenderArgs A
           begin_frame();
         }
 #ifdef MCPT_PHASE_TIMING
-        n_started += (uint64_t)__popcll(__ballot(ready));
+        if (ready) {
+          n_started++, rt_last = __builtin_amdgcn_s_memrealtime();
+          if (A.entry_log) A.entry_log[((size_t)pp * A.blocks + blk) * 3 + 1] = (uint32_t)rt_last;
+        } else {
+          pend_it++;
+        }
 #endif
       }
     }
@@ -1059,6 +1083,7 @@ __global__ void __launch_bounds__(64, MCPT_WAVES_PER_SIMD) k_render(RenderArgs A
     ++w_it_log;
 #endif
     const bool live = G ? lst <= kBusy : lst == kBusy;  // (kRes only with glossy materials)
+    if (STATS || PRIM) px_it += live;
     // phase thresholds scaled to the wave's live lanes: a wave with few pixels
     // (a launch's tail, a strong-scaled rank) does not wait for lane counts
     // only a full wave reaches (C2 -3 %, C5 -4 %, C2 4- and 8-rank shares
@@ -1232,6 +1257,8 @@ __global__ void __launch_bounds__(64, MCPT_WAVES_PER_SIMD) k_render(RenderArgs A
         const f4 v = U->cam.camera_type == 0 ? d : o;
         h.ray[0] = v.x, h.ray[1] = v.y, h.ray[2] = v.z;
         A.prim_out[(size_t)(pxy >> 16) * (size_t)A.W + (pxy & 0xFFFFu)] = h;
+        A.prim_cost[(size_t)(pxy >> 16) * (size_t)A.W + (pxy & 0xFFFFu)] = px_it;
+        px_it = 0;
         lst = kNeed;
       } else if (in_s) {
         if (STATS && lst == kBusy) n_seg++, px_seg++;
@@ -1290,6 +1317,11 @@ __global__ void __launch_bounds__(64, MCPT_WAVES_PER_SIMD) k_render(RenderArgs A
               A.count[pid] = cnt;
             }
             if (STATS && A.px_segments) atomicAdd(A.px_segments + pid, px_seg);
+            if (STATS && A.px_iters) atomicAdd(A.px_iters + pid, px_it);
+            if (STATS) px_it = 0;
+#ifdef MCPT_PHASE_TIMING
+            if (A.entry_log) A.entry_log[((size_t)pid * A.blocks + blk) * 3 + 2] = (uint32_t)__builtin_amdgcn_s_memrealtime();
+#endif
             if (STATS) px_seg = 0;
             lst = kNeed;
           }
@@ -1308,20 +1340,29 @@ __global__ void __launch_bounds__(64, MCPT_WAVES_PER_SIMD) k_render(RenderArgs A
   if (lane == 0)
     for (int k = 0; k < 4; ++k) atomicAdd(&A.stats[kPhaseSlot + k], (unsigned long long)ph[k]);
   {
-    // the earliest lane's dry time (lanes record it in their own registers)
-    uint64_t dry = rt_dry ? rt_dry : ~0ull;
-    for (int off = 32; off > 0; off >>= 1) {
-      const uint64_t o2 = ((uint64_t)(uint32_t)__shfl_xor((int)(uint32_t)(dry >> 32), off) << 32) |
-                          (uint32_t)__shfl_xor((int)(uint32_t)dry, off);
-      dry = o2 < dry ? o2 : dry;
-    }
+    // wave reductions of the lanes' records: earliest dry time, latest
+    // entry start, entries started, iterations spent waiting for a block
+    auto red = [&](uint64_t v, int op) {  // 0 min, 1 max, 2 sum
+      for (int off = 32; off > 0; off >>= 1) {
+        const uint64_t o2 = ((uint64_t)(uint32_t)__shfl_xor((int)(uint32_t)(v >> 32), off) << 32) |
+                            (uint32_t)__shfl_xor((int)(uint32_t)v, off);
+        v = op == 0 ? (o2 < v ? o2 : v) : (op == 1 ? (o2 > v ? o2 : v) : v + o2);
+      }
+      return v;
+    };
+    const uint64_t dry = red(rt_dry ? rt_dry : ~0ull, 0);
+    const uint64_t last = red(rt_last, 1), started = red(n_started, 2), pend = red(pend_it, 2);
     const uint64_t rt_end = __builtin_amdgcn_s_memrealtime();
     if (A.wave_log && lane == 0) {
-      unsigned long long *w = A.wave_log + (size_t)blockIdx.x * 4;
+      unsigned long long *w = A.wave_log + (size_t)blockIdx.x * kWaveLogWords;
       w[0] = rt_start;
       w[1] = dry == ~0ull ? rt_end : dry;
       w[2] = rt_end;
-      w[3] = (w_it_log << 32) | (n_started & 0xFFFFFFFFull);
+      w[3] = w_it_log;
+      w[4] = started;
+      w[5] = last ? last : rt_start;
+      w[6] = pend;
+      w[7] = xcc_id();
     }
   }
 #endif
@@ -1415,6 +1456,47 @@ __global__ void __launch_bounds__(64) k_primary(RenderArgs A, PrimHit *out) {
   const f4 v = A.cam.camera_type == 0 ? d : o;
   h.ray[0] = v.x, h.ray[1] = v.y, h.ray[2] = v.z;
   out[(size_t)y * A.W + x] = h;
+  A.prim_cost[(size_t)y * A.W + x] = tr.nodes + tr.tests;
+}
+
+// The dearest-first tile order (mcpt_tuning.tile_order): each 8x8 tile of
+// the rank's rows keyed by its pixels' primary-ray traversal cost (the
+// costliest pixel, or the sum), sorted descending (hipcub), so the tiles
+// whose pixel chains take longest are claimed first.  Speed only: which lane
+// runs which entry when never changes a bit.
+constexpr int kTileBuckets = 256;  // tile-order keys: the cost saturated to 8 bits
+__global__ void __launch_bounds__(64) k_tile_keys(RenderArgs A, const uint32_t *cost, int32_t n_tiles, int sum,
+                                                  uint8_t *keys) {
+  // one wave per tile, one lane per pixel
+  const int32_t t = (int32_t)blockIdx.x;
+  const int k = (int)threadIdx.x;
+  const int32_t x = (t % A.tiles_x) * 8 + (k & 7), lr = (t / A.tiles_x) * 8 + (k >> 3);
+  uint32_t c = x < A.W && lr < A.local_rows ? cost[(size_t)global_row(lr, A) * A.W + x] : 0u;
+  for (int off = 32; off > 0; off >>= 1) {
+    const uint32_t o = (uint32_t)__shfl_xor((int)c, off);
+    c = sum ? c + o : max(c, o);
+  }
+  if (sum) c = (c + 7u) >> 3;  // the summed cost in units of 8
+  if (k == 0) keys[t] = (uint8_t)min(c, (uint32_t)(kTileBuckets - 1));
+}
+// Counting sort of the tile keys, dearest first, in one workgroup (tiles in
+// a bucket keep no particular order: speed only).
+__global__ void __launch_bounds__(1024) k_tile_sort(const uint8_t *keys, int32_t n_tiles, int32_t *order) {
+  __shared__ uint32_t hist[kTileBuckets];
+  for (int b = threadIdx.x; b < kTileBuckets; b += blockDim.x) hist[b] = 0;
+  __syncthreads();
+  for (int32_t t = threadIdx.x; t < n_tiles; t += blockDim.x) atomicAdd(&hist[kTileBuckets - 1 - keys[t]], 1u);
+  __syncthreads();
+  if (threadIdx.x == 0) {  // exclusive scan of 256 counters
+    uint32_t run = 0;
+    for (int b = 0; b < kTileBuckets; ++b) {
+      const uint32_t c = hist[b];
+      hist[b] = run;
+      run += c;
+    }
+  }
+  __syncthreads();
+  for (int32_t t = threadIdx.x; t < n_tiles; t += blockDim.x) order[atomicAdd(&hist[kTileBuckets - 1 - keys[t]], 1u)] = t;
 }
 
 __global__ void k_shade(const mcpt_material *mats, mcpt_ray *rays, const mcpt_hit *hits, f4 *colors,
@@ -1518,7 +1600,11 @@ int mcpt_ctx_destroy(mcpt_ctx *c) {
   if (c->d_handoff) (void)hipFree(c->d_handoff);
   if (c->d_spill) (void)hipFree(c->d_spill);
   if (c->d_prim) (void)hipFree(c->d_prim);
+  if (c->d_prim_cost) (void)hipFree(c->d_prim_cost);
+  if (c->d_tile_order) (void)hipFree(c->d_tile_order);
+  if (c->d_tile_key) (void)hipFree(c->d_tile_key);
   if (c->d_wave_log) (void)hipFree(c->d_wave_log);
+  if (c->d_entry_log) (void)hipFree(c->d_entry_log);
   if (c->ev0) (void)hipEventDestroy(c->ev0);
   if (c->ev1) (void)hipEventDestroy(c->ev1);
   if (c->ev_prim) (void)hipEventDestroy(c->ev_prim);
@@ -1657,9 +1743,21 @@ int mcpt_set_stats(mcpt_ctx *c, int32_t on) {
   return MCPT_OK;
 }
 
-int mcpt_set_pixel_segments(mcpt_ctx *c, uint32_t *counts_dev) {
+int mcpt_set_pixel_segments(mcpt_ctx *c, uint32_t *counts_dev, uint32_t *iters_dev) {
   if (!c) return mcpt::fail(MCPT_ERR_ARG, "set_pixel_segments: null ctx");
   c->px_segments = counts_dev;
+  c->px_iters = iters_dev;
+  return MCPT_OK;
+}
+
+int mcpt_get_primary_cost(mcpt_ctx *c, uint32_t *out, int64_t cap, int64_t *n) {
+  if (!c || !n) return mcpt::fail(MCPT_ERR_ARG, "get_primary_cost: null");
+  *n = c->prim_valid ? (int64_t)c->prim_key.w * c->prim_key.h : 0;
+  if (!out || *n == 0) return MCPT_OK;
+  if (cap < *n) return mcpt::fail(MCPT_ERR_ARG, "get_primary_cost: buffer too small");
+  HIP_OK(hipSetDevice(c->device));
+  if (c->last_pending) HIP_OK(hipEventSynchronize(c->ev1));
+  HIP_OK(hipMemcpy(out, c->d_prim_cost, (size_t)*n * sizeof(uint32_t), hipMemcpyDeviceToHost));
   return MCPT_OK;
 }
 
@@ -1706,7 +1804,19 @@ int mcpt_get_wave_log(mcpt_ctx *c, uint64_t *out, int64_t cap_workgroups, int64_
   if (cap_workgroups < c->wave_log_n) return mcpt::fail(MCPT_ERR_ARG, "get_wave_log: buffer too small");
   HIP_OK(hipSetDevice(c->device));
   if (c->last_pending) HIP_OK(hipEventSynchronize(c->ev1));
-  HIP_OK(hipMemcpy(out, c->d_wave_log, (size_t)c->wave_log_n * 4 * sizeof(uint64_t), hipMemcpyDeviceToHost));
+  HIP_OK(hipMemcpy(out, c->d_wave_log, (size_t)c->wave_log_n * kWaveLogWords * sizeof(uint64_t), hipMemcpyDeviceToHost));
+  return MCPT_OK;
+}
+
+int mcpt_get_entry_log(mcpt_ctx *c, uint32_t *out, int64_t cap_entries, int64_t *n_entries, int32_t *blocks) {
+  if (!c || !n_entries) return mcpt::fail(MCPT_ERR_ARG, "get_entry_log: null");
+  *n_entries = c->entry_log_n;
+  if (blocks) *blocks = c->entry_log_blocks;
+  if (!out || c->entry_log_n == 0) return MCPT_OK;
+  if (cap_entries < c->entry_log_n) return mcpt::fail(MCPT_ERR_ARG, "get_entry_log: buffer too small");
+  HIP_OK(hipSetDevice(c->device));
+  if (c->last_pending) HIP_OK(hipEventSynchronize(c->ev1));
+  HIP_OK(hipMemcpy(out, c->d_entry_log, (size_t)c->entry_log_n * 3 * sizeof(uint32_t), hipMemcpyDeviceToHost));
   return MCPT_OK;
 }
 
@@ -1715,7 +1825,7 @@ int mcpt_set_tuning(mcpt_ctx *c, const mcpt_tuning *t) {
   if (t && (t->stack_window < 0 || t->stack_window > 2 || t->quantized < 0 || t->quantized > 2 ||
             t->primary_cache < 0 || t->primary_cache > 2 || t->lds_pad < 0 || t->lds_pad > 65536 ||
             t->queue_chunk > 4096 || t->leaf_threshold > 64 || t->shade_threshold > 64 || t->fetch_threshold > 64 ||
-            t->last_block_frames < -1))
+            t->last_block_frames < -1 || t->tile_order < 0 || t->tile_order > 2))
     return mcpt::fail(MCPT_ERR_ARG, "set_tuning: value out of range");
   if (t)
     c->tune = *t;
@@ -2389,17 +2499,35 @@ int mcpt_render_frames(mcpt_ctx *ctx, const mcpt_scene *scene, const mcpt_camera
   A.spill = ctx->d_spill;
   A.wave_log = nullptr;
   A.px_segments = ctx->stats_on ? ctx->px_segments : nullptr;
+  A.px_iters = ctx->stats_on ? ctx->px_iters : nullptr;
+  A.prim_cost = nullptr;  // set where the primary-hit pass runs
   ctx->wave_log_n = 0;
   if (kTiming) {  // diagnostics: each launch's workgroups log their timeline (the last launch's remain)
     if (grid > ctx->wave_log_cap) {
       if (ctx->d_wave_log) HIP_OK(hipFree(ctx->d_wave_log));
       ctx->d_wave_log = nullptr;
       ctx->wave_log_cap = 0;
-      HIP_OK(hipMalloc(&ctx->d_wave_log, (size_t)grid * 4 * sizeof(unsigned long long)));
+      HIP_OK(hipMalloc(&ctx->d_wave_log, (size_t)grid * kWaveLogWords * sizeof(unsigned long long)));
       ctx->wave_log_cap = grid;
     }
     A.wave_log = ctx->d_wave_log;
     ctx->wave_log_n = grid;
+  }
+  A.entry_log = nullptr;
+  ctx->entry_log_n = 0;
+  if (kTiming && n_launch == 1 && (int64_t)p->width * p->height * n_blocks_all <= (16ll << 20)) {
+    const int64_t need = (int64_t)p->width * p->height * n_blocks_all;
+    if (need > ctx->entry_log_cap) {
+      if (ctx->d_entry_log) HIP_OK(hipFree(ctx->d_entry_log));
+      ctx->d_entry_log = nullptr;
+      ctx->entry_log_cap = 0;
+      HIP_OK(hipMalloc(&ctx->d_entry_log, (size_t)need * 3 * sizeof(uint32_t)));
+      ctx->entry_log_cap = need;
+    }
+    HIP_OK(hipMemsetAsync(ctx->d_entry_log, 0, (size_t)need * 3 * sizeof(uint32_t), st));
+    A.entry_log = ctx->d_entry_log;
+    ctx->entry_log_n = need;
+    ctx->entry_log_blocks = (int32_t)n_blocks_all;
   }
   if (ctx->stats_on || kDebug || kTiming)
     HIP_OK(hipMemsetAsync(ctx->d_stats, 0, kStatSlots * sizeof(unsigned long long), st));
@@ -2411,6 +2539,7 @@ int mcpt_render_frames(mcpt_ctx *ctx, const mcpt_scene *scene, const mcpt_camera
   // never.  Speed only: the same bits either way.
   A.prim = nullptr;
   A.prim_out = nullptr;
+  A.tile_order = nullptr;
   int prim_state = 0;
   if (T.primary_cache != 2 && tiles > 0 && p->frames > 0) {
     PrimKey key;
@@ -2433,11 +2562,15 @@ int mcpt_render_frames(mcpt_ctx *ctx, const mcpt_scene *scene, const mcpt_camera
         if (n_px > ctx->prim_cap) {
           ctx->prim_valid = false;
           if (ctx->d_prim) HIP_OK(hipFree(ctx->d_prim));
+          if (ctx->d_prim_cost) HIP_OK(hipFree(ctx->d_prim_cost));
           ctx->d_prim = nullptr;
+          ctx->d_prim_cost = nullptr;
           ctx->prim_cap = 0;
           HIP_OK(hipMalloc(&ctx->d_prim, (size_t)n_px * sizeof(PrimHit)));
+          HIP_OK(hipMalloc(&ctx->d_prim_cost, (size_t)n_px * sizeof(uint32_t)));
           ctx->prim_cap = n_px;
         }
+        A.prim_cost = ctx->d_prim_cost;
         if (scene->near4_bytes <= kPrimSmallTree) {
           // small trees: one ray per lane, one 8x8 tile per workgroup
           const size_t lds_p = (size_t)depth_entries * 64 * sizeof(int32_t);
@@ -2461,6 +2594,8 @@ int mcpt_render_frames(mcpt_ctx *ctx, const mcpt_scene *scene, const mcpt_camera
           Ap.prim_out = ctx->d_prim;
           Ap.wave_log = nullptr;
           Ap.px_segments = nullptr;
+          Ap.px_iters = nullptr;
+          Ap.entry_log = nullptr;
           Ap.queue = ctx->d_queue + (size_t)n_launch * kQueues * kQueueStride;
           HIP_OK(hipMemsetAsync(Ap.queue, 0, (size_t)kQueues * kQueueStride * sizeof(uint32_t), st));
           // its own resident grid: the PRIM form needs fewer registers
@@ -2484,10 +2619,35 @@ int mcpt_render_frames(mcpt_ctx *ctx, const mcpt_scene *scene, const mcpt_camera
         }
         HIP_OK(hipEventRecord(ctx->ev_prim, st));
         ctx->prim_key = key;
+        ctx->tile_order_mode = 0;  // a new cache: the tile order is rebuilt from its costs
         ctx->prim_valid = true;
       }
       A.prim = ctx->d_prim;
       prim_state = have ? 1 : 2;
+      // the dearest-first tile order, built from the pass's per-pixel costs
+      // once per primary-hit cache (and order mode)
+      const int32_t mode = T.tile_order == 0 ? 1 : T.tile_order;  // 1 max, 2 sum (tuning value 1: off)
+      if (T.tile_order != 1) {
+        if (!have || ctx->tile_order_mode != mode) {
+          if (tiles > ctx->tile_cap) {
+            if (ctx->d_tile_order) HIP_OK(hipFree(ctx->d_tile_order));
+            if (ctx->d_tile_key) HIP_OK(hipFree(ctx->d_tile_key));
+            ctx->d_tile_order = nullptr;
+            ctx->d_tile_key = nullptr;
+            ctx->tile_cap = 0;
+            HIP_OK(hipMalloc(&ctx->d_tile_order, (size_t)tiles * sizeof(int32_t)));
+            HIP_OK(hipMalloc(&ctx->d_tile_key, (size_t)tiles));
+            ctx->tile_cap = tiles;
+          }
+          hipLaunchKernelGGL(k_tile_keys, dim3((unsigned)tiles), dim3(64), 0, st, A, ctx->d_prim_cost, (int32_t)tiles,
+                             mode == 2 ? 1 : 0, ctx->d_tile_key);
+          hipLaunchKernelGGL(k_tile_sort, dim3(1), dim3(1024), 0, st, ctx->d_tile_key, (int32_t)tiles,
+                             ctx->d_tile_order);
+          HIP_OK(hipGetLastError());
+          ctx->tile_order_mode = mode;
+        }
+        A.tile_order = ctx->d_tile_order;
+      }
     }
   }
   int launches = 0;

@@ -143,28 +143,50 @@ class Renderer:
         out["phase_ticks"] = list(out["phase_ticks"])
         return out
 
-    def set_pixel_segments(self, counts):
+    def set_pixel_segments(self, counts, iters=None):
         """mcpt_set_pixel_segments: with stats on, render calls add each pixel's
-        segments into `counts` (an int32 CUDA tensor of width*height, zeroed by
-        the caller); None stops it."""
-        self._px_counts = counts  # kept alive while the library holds the pointer
-        L.check(L.lib().mcpt_set_pixel_segments(self.ctx, None if counts is None else L.ptr(counts)))
+        segments into `counts` and its busy loop iterations into `iters` (int32
+        CUDA tensors of width*height, zeroed by the caller; None: not
+        collected)."""
+        self._px_counts = (counts, iters)  # kept alive while the library holds the pointers
+        L.check(L.lib().mcpt_set_pixel_segments(self.ctx, None if counts is None else L.ptr(counts),
+                                                None if iters is None else L.ptr(iters)))
+
+    def primary_cost(self):
+        """mcpt_get_primary_cost: the cached view's per-pixel primary-ray
+        traversal cost (uint32, width*height), or None without a cache."""
+        n = ctypes.c_int64()
+        L.check(L.lib().mcpt_get_primary_cost(self.ctx, None, 0, ctypes.byref(n)))
+        if n.value == 0:
+            return None
+        out = np.zeros(n.value, np.uint32)
+        L.check(L.lib().mcpt_get_primary_cost(self.ctx, L.ptr(out), n.value, ctypes.byref(n)))
+        return out
 
     def wave_log(self):
         """mcpt_get_wave_log (MCPT_PHASE_TIMING library only): per workgroup of
-        the last launch, (start, first-dry, end) in 100 MHz ticks and (iterations,
-        entries started) as an (n, 5) int64 array; empty on release builds."""
+        the last launch an int64 row (start, first dry, end, last entry start
+        [100 MHz ticks], iterations, entries started, lane-iterations waiting,
+        XCD); an empty (0, 8) array on release builds."""
         n = ctypes.c_int64()
         L.check(L.lib().mcpt_get_wave_log(self.ctx, None, 0, ctypes.byref(n)))
         if n.value == 0:
-            return np.zeros((0, 5), np.int64)
-        buf = np.zeros((n.value, 4), np.uint64)
+            return np.zeros((0, 8), np.int64)
+        buf = np.zeros((n.value, 8), np.uint64)
         L.check(L.lib().mcpt_get_wave_log(self.ctx, L.ptr(buf), n.value, ctypes.byref(n)))
-        out = np.zeros((n.value, 5), np.int64)
-        out[:, :3] = buf[:, :3].astype(np.int64)
-        out[:, 3] = (buf[:, 3] >> np.uint64(32)).astype(np.int64)
-        out[:, 4] = (buf[:, 3] & np.uint64(0xFFFFFFFF)).astype(np.int64)
-        return out
+        return buf[:, [0, 1, 2, 5, 3, 4, 6, 7]].astype(np.int64)
+
+    def entry_log(self):
+        """mcpt_get_entry_log (MCPT_PHASE_TIMING library only): (pixels, blocks, 3)
+        uint32 claim / start / end times (100 MHz ticks, low 32 bits) of the
+        last one-launch call's queue entries; None when nothing was logged."""
+        n, b = ctypes.c_int64(), ctypes.c_int32()
+        L.check(L.lib().mcpt_get_entry_log(self.ctx, None, 0, ctypes.byref(n), ctypes.byref(b)))
+        if n.value == 0:
+            return None
+        buf = np.zeros((n.value, 3), np.uint32)
+        L.check(L.lib().mcpt_get_entry_log(self.ctx, L.ptr(buf), n.value, ctypes.byref(n), ctypes.byref(b)))
+        return buf.reshape(-1, b.value, 3)
 
     def set_tuning(self, **knobs):
         """mcpt_set_tuning: k_render launch-plan knobs (leaf_threshold,
@@ -242,21 +264,25 @@ class Renderer:
         in scene.schedule.  Both schedules give bit-identical images, so this
         only moves speed.  Returns (schedule, {schedule: best ms})."""
         sched, _, best = self.tune(scene, camera, state, max_depth, max_attempt, frames, trials, shade_thresholds=None,
-                                   fetch_thresholds=None, **kw)
+                                   fetch_thresholds=None, tile_orders=None, **kw)
         return sched, {k[0]: v for k, v in best.items()}
 
     def tune(self, scene, camera, state, max_depth, max_attempt, frames=64, trials=1, shade_thresholds=(32, 40, 48),
-             fetch_thresholds=(1, 8), block_entries=(8, 16), last_block=True, **kw):
+             fetch_thresholds=(1, 8), block_entries=(8, 16), last_block=True, tile_orders=(0, 1, 2), **kw):
         """tune_schedule over the leaf-test schedule, the S-phase threshold
         (mcpt_tuning.shade_threshold) and then the fetch threshold
         (mcpt_tuning.fetch_threshold), then the block sizing
-        (mcpt_tuning.block_entries), then a short last block against equal
-        blocks (mcpt_tuning.last_block_frames -1 or ceil(frames / 8); the
-        auto rule's value is kept when it is as fast): their best values differ by scene
-        (round 2, 3-frame blocks: veach_mis S 40, fetch 8; cbox S 32-40, fetch 8;
-        the 10 M-triangle soup S 32, fetch 1).  Every combination gives the same bits.  The
-        winner goes to scene.schedule and the renderer's tuning.  Returns
-        (schedule, shade_threshold, {(schedule, shade, fetch, entries): best ms})."""
+        (mcpt_tuning.block_entries) jointly with the tile order
+        (mcpt_tuning.tile_order: dearest tiles first by their costliest or
+        summed primary-ray cost, or image order), then a short last block
+        against equal blocks (mcpt_tuning.last_block_frames -1 or
+        ceil(frames / 8)); ties keep the baseline value.  Their best values
+        differ by scene (round 2, 3-frame blocks: veach_mis S 40, fetch 8;
+        cbox S 32-40, fetch 8; the 10 M-triangle soup S 32, fetch 1; round 4:
+        cbox gains 5-10 % from the dearest-first order, veach_mis loses 5 %).
+        Every combination gives the same bits.  The winner goes to
+        scene.schedule and the renderer's tuning.  Returns (schedule,
+        shade_threshold, {(schedule, shade, fetch, entries, tile_order): best ms})."""
         if getattr(self, "_stats_on", False):
             raise L.MCPTError("tune: counters must be off (they change the kernel)")
         base = self.get_tuning()
@@ -265,49 +291,57 @@ class Renderer:
         scratch.width, scratch.height, scratch.frames_done = state.width, state.height, state.frames_done
         best = {}
 
-        def trial(sched, th, fe, be):
-            self.set_tuning(**dict(base, shade_threshold=th, fetch_threshold=fe, block_entries=be))
+        def trial(sched, th, fe, be, to):
+            self.set_tuning(**dict(base, shade_threshold=th, fetch_threshold=fe, block_entries=be, tile_order=to))
             scratch.seeds, scratch.hist, scratch.count = state.seeds.clone(), state.hist.clone(), state.count.clone()
             self.render_frames(scene, camera, scratch, max_depth, max_attempt, frames,
                                frame_begin=state.frames_done, schedule=sched, **kw)
             ms = self.stats()["kernel_ms"]
-            best[(sched, th, fe, be)] = min(best.get((sched, th, fe, be), ms), ms)
+            key = (sched, th, fe, be, to)
+            best[key] = min(best.get(key, ms), ms)
+
+        def pick():  # fastest; ties to the smaller key
+            return min(best, key=lambda k: (best[k], k))
 
         fe0 = base["fetch_threshold"] or 1  # 0 = the default, 1
         be0 = base["block_entries"] or 8    # 0 = the default, 8
+        to0 = base["tile_order"]
         try:
             for _ in range(int(trials)):
                 for th in ths:
                     for sched in (L.SCHED_SINGLE, L.SCHED_PAIRED):
-                        trial(sched, th, fe0, be0)
-            sched, th, fe, be = min(best, key=lambda k: (best[k], k))
+                        trial(sched, th, fe0, be0, to0)
+            sched, th, fe, be, to = pick()
             if shade_thresholds and fetch_thresholds:  # then the fetch threshold, with that pair
                 for _ in range(int(trials)):
                     for f in fetch_thresholds:
                         if f != fe0:
-                            trial(sched, th, f, be0)
-                sched, th, fe, be = min(best, key=lambda k: (best[k], k))
-            if shade_thresholds and block_entries:  # then the block sizing
+                            trial(sched, th, f, be0, to0)
+                sched, th, fe, be, to = pick()
+            if shade_thresholds and (block_entries or tile_orders):  # then block sizing x tile order
+                bes = list(block_entries) if block_entries else [be0]
+                tos = list(tile_orders) if tile_orders else [to0]
                 for _ in range(int(trials)):
-                    for b in block_entries:
-                        if b != be0:
-                            trial(sched, th, fe, b)
-                sched, th, fe, be = min(best, key=lambda k: (best[k], k))
-                if be != be0:  # other blocks move the best S threshold (C3: 48 -> 40)
+                    for b in bes:
+                        for o in tos:
+                            if (b, o) != (be0, to0):
+                                trial(sched, th, fe, b, o)
+                sched, th, fe, be, to = pick()
+                if (be, to) != (be0, to0):  # other blocks or orders move the best S threshold (C3: 48 -> 40)
                     for _ in range(int(trials)):
                         for t in ths:
                             if t != th:
-                                trial(sched, t, fe, be)
-                    sched, th, fe, be = min(best, key=lambda k: (best[k], k))
+                                trial(sched, t, fe, be, to)
+                    sched, th, fe, be, to = pick()
             lb = base["last_block_frames"]
             if shade_thresholds and last_block:  # then a short last block against equal blocks
                 lbs = {-1, (int(frames) + 7) // 8}
-                key = (sched, th, fe, be)
+                key = (sched, th, fe, be, to)
                 lbest = {lb: best[key]}
                 for _ in range(int(trials)):
                     for v in sorted(lbs - {lb}):
                         self.set_tuning(**dict(base, shade_threshold=th, fetch_threshold=fe, block_entries=be,
-                                               last_block_frames=v))
+                                               tile_order=to, last_block_frames=v))
                         scratch.seeds, scratch.hist, scratch.count = (state.seeds.clone(), state.hist.clone(),
                                                                       state.count.clone())
                         self.render_frames(scene, camera, scratch, max_depth, max_attempt, frames,
@@ -321,7 +355,7 @@ class Renderer:
         scene.schedule = sched
         if shade_thresholds:
             self.set_tuning(**dict(base, shade_threshold=th, fetch_threshold=fe, block_entries=be,
-                                   last_block_frames=lb))
+                                   last_block_frames=lb, tile_order=to))
         return sched, th, best
 
     # ------------------------------------------------ wavefront (drop-in)

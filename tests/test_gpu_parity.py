@@ -400,15 +400,17 @@ def test_exact_equals_noprune_full_size(rnd):
 def test_launch_knobs_change_no_bits_full_size(rnd):
     """Size-independent property at a C2-like configuration: every launch-plan
     knob Renderer.tune and bench.py set (S-phase and fetch thresholds, leaf
-    threshold, queue chunk, block sizing, queue count) moves only speed: the
-    image, counts and seed chains are identical for each setting."""
+    threshold, queue chunk, block sizing, queue count, the dearest-first tile
+    order) moves only speed: the image, counts and seed chains are identical
+    for each setting."""
     data, cam = scenes.cbox_diffuse(), S.parse_camera(scenes.CBOX_CAM)
     w = h = 256
     seeds = R.default_seeds(w * h)
     dsc = rnd.upload(data)
     settings = [{}, {"shade_threshold": 48, "fetch_threshold": 8}, {"shade_threshold": 24, "leaf_threshold": 8},
                 {"fetch_threshold": 64, "queue_chunk": 16}, {"block_entries": 4, "max_block_frames": 2},
-                {"queues": 1}, {"queues": 3, "fetch_threshold": 5}, {"primary_cache": 2}, {"primary_cache": 1}]
+                {"queues": 1}, {"queues": 3, "fetch_threshold": 5}, {"primary_cache": 2}, {"primary_cache": 1},
+                {"tile_order": 1}, {"tile_order": 2}, {"tile_order": 2, "queues": 3}]
     outs = []
     try:
         for t in settings:
@@ -591,10 +593,11 @@ def test_tune_schedule_leaves_state_alone(rnd):
     sched, th, best2 = rnd.tune(dsc, cam, st2, 12, 1 << 20, frames=4, trials=1)
     try:
         assert th in (32, 40, 48) and rnd.get_tuning()["shade_threshold"] == th and dsc.schedule == sched
-        # 3 S thresholds x 2 schedules, the other fetch threshold, the other block sizing, and
-        # the other two S thresholds again when the block sizing changed
-        assert len(best2) in (8, 10) and int(st2.count.sum()) == 0
+        # 3 S thresholds x 2 schedules, the other fetch threshold, the other 5 (block sizing, tile
+        # order) pairs, and the other two S thresholds again when that pair changed
+        assert len(best2) in (12, 14) and int(st2.count.sum()) == 0
         assert (rnd.get_tuning()["block_entries"] or 8) in (8, 16)
+        assert rnd.get_tuning()["tile_order"] in (0, 1, 2)
         assert rnd.get_tuning()["last_block_frames"] in (-1, 0, 1)  # equal, auto, or ceil(4 / 8)
         rnd.render_frames(dsc, cam, st2, 12, 1 << 20, 6)
         torch.cuda.synchronize()

@@ -43,13 +43,16 @@ def main():
     dsc.schedule = L.SCHED_PAIRED
     st = rnd.new_state(w, h)
     counts = torch.zeros(w * h, dtype=torch.int32, device=rnd.device)
+    iters = torch.zeros(w * h, dtype=torch.int32, device=rnd.device)
     rnd.set_stats(True)
-    rnd.set_pixel_segments(counts)
+    rnd.set_pixel_segments(counts, iters)
     rnd.render_frames(dsc, cam, st, wl["depth"], 1 << 30, a.frames)
     s = rnd.stats()
     rnd.set_pixel_segments(None)
     rnd.set_stats(False)
     c = counts.cpu().numpy().astype(np.int64)
+    it = iters.cpu().numpy().astype(np.int64)
+    pc = rnd.primary_cost()
     lanes = s["workgroups"] * 64
     assert int(c.sum()) == int(s["segments"]), (int(c.sum()), s["segments"])
     rec = {"workload": a.workload, "frames": a.frames, "pixels": w * h, "segments": int(c.sum()),
@@ -66,6 +69,20 @@ def main():
                        "bound": "chain" if cs.max() > load else "load",
                        "share_time_floor_vs_1gpu": round(float(max(load, cs.max()) / (c.sum() / float(lanes))), 4)})
     rec["shares"] = shares
+    # how well the primary ray's own traversal cost predicts the chain's loop
+    # iterations (the time a pixel's frames take at a given load)
+    rec["iters_per_pixel_mean_p50_p99_max"] = [round(float(it.mean()), 1)] + [int(np.percentile(it, q)) for q in (50, 99)] + [int(it.max())]
+    if pc is not None:
+        pc = pc.astype(np.int64)
+        rec["primary_cost_mean_p50_p99_max"] = [round(float(pc.mean()), 2)] + [int(np.percentile(pc, q)) for q in (50, 99)] + [int(pc.max())]
+        rec["corr_primary_cost_vs_chain_iters"] = round(float(np.corrcoef(pc, it)[0, 1]), 4)
+        top = np.argsort(it)[-1000:]  # the 1000 slowest chains
+        for frac in (0.01, 0.05, 0.1):
+            k = int(frac * len(pc))
+            hot = np.argsort(pc, kind="stable")[-k:]
+            rec["slowest1000_in_top%d%%_primary_cost" % int(frac * 100)] = int(np.isin(top, hot).sum())
+        np.save(os.path.join(os.path.dirname(a.out), "chain_%s.npy" % a.workload),
+                np.stack([c, it, pc]).astype(np.int32))
     print(json.dumps(rec), flush=True)
     os.makedirs(os.path.dirname(a.out), exist_ok=True)
     with open(a.out, "a") as fh:

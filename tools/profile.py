@@ -79,6 +79,9 @@ def run(tag, args):
                      "--block-entries", str(cfg.get("block_entries", 8))]
     if cfg.get("last_block_frames"):  # 0: the auto rule, which the pinned command keeps (it does not tune)
         quiet += ["--last-block-frames", str(cfg["last_block_frames"])]
+    if "tile_order" in cfg:
+        quiet += ["--tile-order", str({"dearest first (costliest pixel)": 0, "image": 1,
+                                       "dearest first (summed)": 2}[cfg["tile_order"]])]
     sh(["rocprofv3", "--kernel-trace", "--stats", "--output-format", "csv", "-d", os.path.join(out, "trace"), "--"]
        + quiet, os.path.join(out, "trace.log"), 400)
     print("trace done", flush=True)

@@ -49,6 +49,8 @@ def main():
                     "(frames/calls each, stream-async, one sync at the end; the app's update() pattern): "
                     "wall-clock ms over all calls is reported as kernel_ms")
     ap.add_argument("--json", default=None, help="append result lines to this file")
+    ap.add_argument("--drop", action="store_true", help="drop the primary-hit cache before every timed call "
+                    "(the call then runs the primary-hit pass and builds its tile order, as bench.py's timed call does)")
     ap.add_argument("--stripes", default="1", help="comma list of stripe counts: rank 0's share of the image "
                     "(16-row stripes dealt round-robin) rendered alone = one rank of an N-GPU strong-scaled run")
     a = ap.parse_args()
@@ -82,6 +84,8 @@ def main():
                 s = rnd.stats()
                 times[i].append((time.perf_counter() - t0) * 1e3)
             else:
+                if a.drop:
+                    rnd.drop_caches()
                 rnd.render_frames(dsc, cam, st, depth, 1 << 30, a.frames, frames_per_launch=fpl, stripe_count=n)
                 s = rnd.stats()
                 times[i].append(s["kernel_ms"])

@@ -29,7 +29,7 @@ from montecarlopathtracing_amd import scene as S  # noqa: E402
 
 
 def summarize(log, ms):
-    st, dry, end = log[:, 0], log[:, 1], log[:, 2]
+    st, dry, end, last = log[:, 0], log[:, 1], log[:, 2], log[:, 3]
     t0 = st.min()
     us = lambda x: (x - t0) / 100.0  # noqa: E731 - 100 MHz ticks -> us
     first_dry = dry.min()
@@ -38,14 +38,50 @@ def summarize(log, ms):
     # workgroups alive over the tail, sampled on 64 points
     ts = np.linspace(first_dry, end.max(), 64)
     alive = [(end > t).mean() for t in ts]
+    slow = np.argsort(end)[-16:]  # the 16 last workgroups
     return {"kernel_ms": round(ms, 3), "span_us": round(float(span), 1),
             "start_spread_us": round(float(us(st.max())), 1),
             "first_dry_us": round(float(us(first_dry)), 1),
             "tail_us_p50_p90_max": [round(float(np.percentile(tail, q)), 1) for q in (50, 90, 100)],
             "tail_share_of_span": round(float((end.max() - first_dry) / 100.0 / span), 4),
             "alive_mean_over_tail": round(float(np.mean(alive)), 4),
-            "iterations_p50_max": [int(np.percentile(log[:, 3], 50)), int(log[:, 3].max())],
-            "entries_per_wg_mean": round(float(log[:, 4].mean()), 2)}
+            "last_start_after_dry_us_p50_max": [round(float(np.percentile((last - first_dry) / 100.0, 50)), 1),
+                                                round(float(((last - first_dry) / 100.0).max()), 1)],
+            "slowest16_last_start_after_dry_us": [round(float(x), 1) for x in (last[slow] - first_dry) / 100.0],
+            "slowest16_end_after_dry_us": [round(float(x), 1) for x in (end[slow] - first_dry) / 100.0],
+            "slowest16_xcd": [int(x) for x in log[slow, 7]],
+            "iterations_p50_max": [int(np.percentile(log[:, 4], 50)), int(log[:, 4].max())],
+            "entries_per_wg_mean": round(float(log[:, 5].mean()), 2),
+            "wait_lane_iterations_mean_max": [round(float(log[:, 6].mean()), 1), int(log[:, 6].max())],
+            "xcd_end_after_dry_us_max": [round(float(((end[log[:, 7] == x] - first_dry) / 100.0).max()), 1)
+                                         if (log[:, 7] == x).any() else None for x in range(8)]}
+
+
+def entry_summary(el, log):
+    """Per-block timing of the (pixel, block) entries (the timing build's
+    entry log: claim, start, end, low 32 bits of the 100 MHz clock), relative
+    to the first queue-dry moment of the wave log: how long entries waited
+    for their pixel's previous block, how long they ran, and the chains of
+    the pixels that ended last."""
+    dry32 = np.uint32(int(log[:, 1].min()) & 0xFFFFFFFF)
+    rel = ((el.astype(np.int64) - int(dry32) + (1 << 31)) % (1 << 32) - (1 << 31)) / 100.0  # us from first dry
+    claim, start, end = rel[..., 0], rel[..., 1], rel[..., 2]
+    nb = el.shape[1]
+    out = {"blocks": nb, "per_block": []}
+    for b in range(nb):
+        w = start[:, b] - claim[:, b]
+        d = end[:, b] - start[:, b]
+        out["per_block"].append({"block": b, "claim_us_p0_p50_p100": [round(float(np.percentile(claim[:, b], q)), 1) for q in (0, 50, 100)],
+                                 "wait_us_p50_p99_max": [round(float(np.percentile(w, q)), 1) for q in (50, 99, 100)],
+                                 "run_us_p50_p99_max": [round(float(np.percentile(d, q)), 1) for q in (50, 99, 100)],
+                                 "end_us_p50_p99_max": [round(float(np.percentile(end[:, b], q)), 1) for q in (50, 99, 100)]})
+    last_end = end.max(axis=1)
+    slow = np.argsort(last_end)[-8:]
+    out["slowest_pixels"] = [{"pixel": int(p), "claim": [round(float(x), 1) for x in claim[p]],
+                              "start": [round(float(x), 1) for x in start[p]],
+                              "end": [round(float(x), 1) for x in end[p]]} for p in slow]
+    out["pixels_ending_after_dry_us_500_800_1200"] = [int((last_end > t).sum()) for t in (500, 800, 1200)]
+    return out
 
 
 def main():
@@ -79,6 +115,12 @@ def main():
                 rec = dict(workload=a.workload, frames=a.frames, fpl=fpl, frames_per_block=s["frames_per_block"],
                            rep=rep, primary_ms=round(s.get("primary_ms", 0.0), 3), **summarize(log, s["kernel_ms"]))
                 print(json.dumps(rec), flush=True)
+                if rep == 0:
+                    np.save(os.path.join(os.path.dirname(a.out), "tail_log_%s_fpl%d.npy" % (a.workload, fpl)), log)
+                    el = rnd.entry_log()
+                    if el is not None:
+                        rec["entries"] = entry_summary(el, log)
+                        print(json.dumps(rec["entries"]), flush=True)
                 fh.write(json.dumps(rec) + "\n")
     dsc.close()
     rnd.close()
