@@ -225,6 +225,14 @@ typedef struct mcpt_tuning {
                                costliest pixel is dearest start first, so the
                                longest per-pixel chains do not start last), 1
                                the image order, 2 by the tile's summed cost    */
+  int32_t pixel_spread;     /* how the queues' pixel slots map to a wave's
+                               lanes: 0 auto (spread up to 2.5 pixels per
+                               resident lane: strong-scaled shares, where each
+                               pixel's own chain sets the time; tile-major
+                               above), 1 tile-major (a wave's 64
+                               consecutive slots are one 8x8 tile), 2 spread
+                               (they are one pixel of each of 64 tiles, so one
+                               tile's dear pixels run in different waves)      */
 } mcpt_tuning;
 
 /* ------------------------------------------------------- version / errors */

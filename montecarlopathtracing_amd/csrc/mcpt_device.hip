@@ -794,6 +794,7 @@ struct RenderArgs {
   uint32_t *prim_cost;        // PRIM launches: each pixel's primary-ray lane-iterations (its traversal cost)
   const int32_t *tile_order;  // queue position -> 8x8 tile (dearest first, mcpt_tuning.tile_order), or nullptr: image order
   uint32_t *entry_log;        // MCPT_PHASE_TIMING: per (pixel, block) claim / start / end times (mcpt_get_entry_log), or nullptr
+  int32_t spread;             // 1: each run of 64 queue slots takes one pixel from each of 64 tiles (mcpt_tuning.pixel_spread)
 };
 
 __device__ inline int32_t global_row(int32_t lr, const RenderArgs &A) {
@@ -1018,7 +1019,18 @@ __global__ void __launch_bounds__(64, MCPT_WAVES_PER_SIMD) k_render(RenderArgs A
           if (got) {
             const uint32_t items = queue_items(qx, n_tiles, nq);
             const uint32_t b = q / items, j = q - b * items;
-            const int32_t tpos = (int32_t)((j >> 6) * nq + qx), k = (int32_t)(j & 63u);
+            uint32_t u = j >> 6, kk = j & 63u;  // the queue's tile u, its pixel kk
+            if (!PRIM && A.spread) {
+              // spread: slot j of the group of (up to) 64 tiles g0.. is pixel
+              // i / gs of tile g0 + i % gs, i = its index in the group, so a
+              // wave's 64 consecutive slots come from 64 tiles and the dear
+              // pixels of one tile run in different waves.  A bijection on the
+              // group's slots, the same for every block of the pixel.
+              const uint32_t g0 = u & ~63u, gs = min(64u, (items >> 6) - g0), i = ((u - g0) << 6) + kk;
+              u = g0 + i % gs;
+              kk = i / gs;
+            }
+            const int32_t tpos = (int32_t)(u * nq + qx), k = (int32_t)kk;
             const int32_t tile = A.tile_order ? A.tile_order[tpos] : tpos;
             const int32_t x = (tile % A.tiles_x) * 8 + (k & 7);
             const int32_t lr = (tile / A.tiles_x) * 8 + (k >> 3);
@@ -1825,7 +1837,8 @@ int mcpt_set_tuning(mcpt_ctx *c, const mcpt_tuning *t) {
   if (t && (t->stack_window < 0 || t->stack_window > 2 || t->quantized < 0 || t->quantized > 2 ||
             t->primary_cache < 0 || t->primary_cache > 2 || t->lds_pad < 0 || t->lds_pad > 65536 ||
             t->queue_chunk > 4096 || t->leaf_threshold > 64 || t->shade_threshold > 64 || t->fetch_threshold > 64 ||
-            t->last_block_frames < -1 || t->tile_order < 0 || t->tile_order > 2))
+            t->last_block_frames < -1 || t->tile_order < 0 || t->tile_order > 2 || t->pixel_spread < 0 ||
+            t->pixel_spread > 2))
     return mcpt::fail(MCPT_ERR_ARG, "set_tuning: value out of range");
   if (t)
     c->tune = *t;
@@ -2413,7 +2426,8 @@ int mcpt_render_frames(mcpt_ctx *ctx, const mcpt_scene *scene, const mcpt_camera
   const int cap = T.max_block_frames > 0 ? T.max_block_frames : 32;  // frames per block at most (auto plans)
   int fpl = p->frames_per_launch;
   bool tail_ok = false;  // auto plan with several entries per lane: a short last block may apply
-  double slots_per_px = 0;  // pixels per resident lane
+  double slots_per_px = 0;  // pixels per resident lane (auto plans)
+  const double px_per_lane = (double)n_items / ((double)std::max(per_cu, 1) * ctx->n_cu * 64);  // vs resident lanes
   if (fpl <= 0) {
     const int frames = std::max(p->frames, 1);
     const double per_block = (double)n_items / (double)(grid * 64);  // entries per lane per block
@@ -2427,7 +2441,7 @@ int mcpt_render_frames(mcpt_ctx *ctx, const mcpt_scene *scene, const mcpt_camera
     // pixels per lane and two up to 2.5 (C2 shares of 4 and 8 ranks, C4 of 8:
     // 1-12 % faster than 4-frame blocks; the C5 8-rank share, 2 pixels per
     // lane: 4 % faster than 5-frame blocks; tools/sweep.py --stripes --fpl)
-    const double per_slot = (double)n_items / ((double)std::max(per_cu, 1) * ctx->n_cu * 64);  // vs resident lanes
+    const double per_slot = px_per_lane;
     slots_per_px = per_slot;
     if (per_slot < 0.75)
       fpl = frames;
@@ -2513,6 +2527,15 @@ int mcpt_render_frames(mcpt_ctx *ctx, const mcpt_scene *scene, const mcpt_camera
     A.wave_log = ctx->d_wave_log;
     ctx->wave_log_n = grid;
   }
+  // pixel_spread auto: spread slots up to 2.5 pixels per resident lane, where
+  // each pixel's own chain sets the time (an N-rank share).  Tile-major slots
+  // put one tile's dear pixels (C2: the pitcher's inside, ~29 loop iterations
+  // per segment) in one wave, whose iterations then run the union of their
+  // phases; spread, they share waves with cheap pixels that finish early.
+  // Slowest share of 8 ranks: C2 5.83 -> 4.20 ms, C4 (64 frames) 58.1 -> 50.9;
+  // 4 ranks: C2 6.51 -> 5.22, C4 76.7 -> 73.0; whole images even (C2, C3, C4,
+  // C5 within 0.7 %; profiles/r04_spread.jsonl).
+  A.spread = T.pixel_spread == 2 || (T.pixel_spread == 0 && px_per_lane <= 2.5) ? 1 : 0;
   A.entry_log = nullptr;
   ctx->entry_log_n = 0;
   if (kTiming && n_launch == 1 && (int64_t)p->width * p->height * n_blocks_all <= (16ll << 20)) {

@@ -410,7 +410,9 @@ def test_launch_knobs_change_no_bits_full_size(rnd):
     settings = [{}, {"shade_threshold": 48, "fetch_threshold": 8}, {"shade_threshold": 24, "leaf_threshold": 8},
                 {"fetch_threshold": 64, "queue_chunk": 16}, {"block_entries": 4, "max_block_frames": 2},
                 {"queues": 1}, {"queues": 3, "fetch_threshold": 5}, {"primary_cache": 2}, {"primary_cache": 1},
-                {"tile_order": 1}, {"tile_order": 2}, {"tile_order": 2, "queues": 3}]
+                {"tile_order": 1}, {"tile_order": 2}, {"tile_order": 2, "queues": 3}, {"pixel_spread": 2},
+                {"pixel_spread": 2, "queues": 3, "block_entries": 4, "max_block_frames": 2},
+                {"pixel_spread": 2, "tile_order": 1, "queues": 5}]
     outs = []
     try:
         for t in settings:
@@ -424,6 +426,34 @@ def test_launch_knobs_change_no_bits_full_size(rnd):
     for t, o in zip(settings[1:], outs[1:]):
         for a, b, what in zip(outs[0], o, ("hist", "count", "seeds")):
             assert_bits_equal(a, b, "%s %s" % (what, t))
+    dsc.close()
+
+
+@pytest.mark.parametrize("wh", [(100, 75), (8, 8), (520, 9)])
+def test_pixel_spread_ragged_images(rnd, wh):
+    """The spread slot mapping (mcpt_tuning.pixel_spread 2: a wave's 64
+    consecutive queue slots are one pixel of each of up to 64 tiles) is a
+    bijection on every queue's slots, partial last groups and edge-tile holes
+    included: ragged images render every pixel exactly as tile-major slots do,
+    with one block per pixel and with several."""
+    data, cam = scenes.cbox_diffuse(), S.parse_camera(scenes.CBOX_CAM)
+    w, h = wh
+    seeds = R.default_seeds(w * h)
+    dsc = rnd.upload(data)
+    outs = []
+    try:
+        for t in ({"pixel_spread": 1}, {"pixel_spread": 2}, {"pixel_spread": 2, "queues": 3},
+                  {"pixel_spread": 2, "block_entries": 64, "max_block_frames": 1}):
+            rnd.set_tuning(**t)
+            st = rnd.new_state(w, h, seeds)
+            rnd.render_frames(dsc, cam, st, 6, 1 << 20, 5)
+            torch.cuda.synchronize()
+            outs.append((st.hist.cpu().numpy(), st.count.cpu().numpy(), st.seeds_np()))
+    finally:
+        rnd.set_tuning()
+    for o in outs[1:]:
+        for a, b, what in zip(outs[0], o, ("hist", "count", "seeds")):
+            assert_bits_equal(a, b, what)
     dsc.close()
 
 

@@ -53,6 +53,9 @@ def main():
                     "(the call then runs the primary-hit pass and builds its tile order, as bench.py's timed call does)")
     ap.add_argument("--stripes", default="1", help="comma list of stripe counts: rank 0's share of the image "
                     "(16-row stripes dealt round-robin) rendered alone = one rank of an N-GPU strong-scaled run")
+    ap.add_argument("--all-ranks", action="store_true", help="with --stripes N: time every rank's share, not "
+                    "only rank 0's; the job's time is the slowest share's (max over ranks)")
+    ap.add_argument("--stripe-rows", type=int, default=16)
     a = ap.parse_args()
     wl = bench.WORKLOADS[a.workload]
     w, h, depth = wl["w"], wl["h"], wl["depth"]
@@ -62,31 +65,31 @@ def main():
     dsc, _ = bench.upload_scene(rnd, data)
     dsc.schedule = L.SCHED_PAIRED if a.schedule == "paired" else L.SCHED_SINGLE
     st = rnd.new_state(w, h)
-    combos = [(fpl, g, n) for n in (int(x) for x in a.stripes.split(",")) for fpl in (int(x) for x in a.fpl.split(","))
-              for g in parse_grid(a.grid)]
+    combos = [(fpl, g, n, r) for n in (int(x) for x in a.stripes.split(",")) for fpl in (int(x) for x in a.fpl.split(","))
+              for g in parse_grid(a.grid) for r in (range(n) if a.all_ranks else (0,))]
     times = {i: [] for i in range(len(combos))}
     ticks = {}
     fpb = {}
-    for i, (fpl, g, n) in enumerate(combos):  # warm every variant once
+    for i, (fpl, g, n, r) in enumerate(combos):  # warm every variant once
         rnd.set_tuning(**g)
-        rnd.render_frames(dsc, cam, st, depth, 1 << 30, min(a.frames, 4), frames_per_launch=fpl, stripe_count=n)
+        rnd.render_frames(dsc, cam, st, depth, 1 << 30, min(a.frames, 4), frames_per_launch=fpl, stripe_count=n, stripe_index=r, stripe_rows=a.stripe_rows)
     torch.cuda.synchronize()
     per_call = max(1, a.frames // max(a.calls, 1))
     for _ in range(a.reps):
-        for i, (fpl, g, n) in enumerate(combos):
+        for i, (fpl, g, n, r) in enumerate(combos):
             rnd.set_tuning(**g)
             if a.calls > 1:
                 torch.cuda.synchronize()
                 t0 = time.perf_counter()
                 for _c in range(a.calls):
-                    rnd.render_frames(dsc, cam, st, depth, 1 << 30, per_call, frames_per_launch=fpl, stripe_count=n)
+                    rnd.render_frames(dsc, cam, st, depth, 1 << 30, per_call, frames_per_launch=fpl, stripe_count=n, stripe_index=r, stripe_rows=a.stripe_rows)
                 torch.cuda.synchronize()
                 s = rnd.stats()
                 times[i].append((time.perf_counter() - t0) * 1e3)
             else:
                 if a.drop:
                     rnd.drop_caches()
-                rnd.render_frames(dsc, cam, st, depth, 1 << 30, a.frames, frames_per_launch=fpl, stripe_count=n)
+                rnd.render_frames(dsc, cam, st, depth, 1 << 30, a.frames, frames_per_launch=fpl, stripe_count=n, stripe_index=r, stripe_rows=a.stripe_rows)
                 s = rnd.stats()
                 times[i].append(s["kernel_ms"])
             fpb[i] = s["frames_per_block"]
@@ -94,7 +97,7 @@ def main():
                 ticks.setdefault(i, [0, 0, 0, 0])
                 ticks[i] = [a + b for a, b in zip(ticks[i], s["phase_ticks"])]
     out = []
-    for i, (fpl, g, n) in enumerate(combos):
+    for i, (fpl, g, n, r) in enumerate(combos):
         ts = sorted(times[i])
         med = ts[len(ts) // 2]
         rec = {"workload": a.workload, "frames": a.frames, "fpl": fpl, "fpb": fpb[i], "tuning": g,
@@ -107,13 +110,13 @@ def main():
             tot = float(sum(ticks[i]))
             rec["phase_frac_fetch_T_L_S"] = [round(t / tot, 4) for t in ticks[i]]
         if n > 1:  # one rank's share: the N-rank job's rate if every rank took as long
-            rec.update({"stripes": n, "Msamples_s": None,
+            rec.update({"stripes": n, "rank": r, "stripe_rows": a.stripe_rows, "Msamples_s": None,
                         "rank0_Msamples_s": round(w * h / n * a.frames * depth / (med / 1e3) / 1e6, 1),
                         "job_Msamples_s_if_balanced": round(w * h * a.frames * depth / (med / 1e3) / 1e6, 1)})
         if a.stats:
             rnd.set_tuning(**g)
             rnd.set_stats(True)
-            rnd.render_frames(dsc, cam, st, depth, 1 << 30, a.frames, frames_per_launch=fpl, stripe_count=n)
+            rnd.render_frames(dsc, cam, st, depth, 1 << 30, a.frames, frames_per_launch=fpl, stripe_count=n, stripe_index=r, stripe_rows=a.stripe_rows)
             c = rnd.stats()
             rnd.set_stats(False)
             seg = max(c["segments"], 1)
@@ -128,6 +131,19 @@ def main():
                         "iters_per_seg": round(c["wave_iterations"] * 64.0 / seg, 3)})
         print(json.dumps(rec), flush=True)
         out.append(rec)
+    if a.all_ranks:  # the job: every rank's share at once, as slow as its slowest
+        for (fpl, g) in {(c[0], json.dumps(c[1], sort_keys=True)) for c in combos}:
+            for n in sorted({c[2] for c in combos}):
+                ms = [r["kernel_ms_median"] for r, c in zip(out, combos) if c[0] == fpl and c[2] == n
+                      and json.dumps(c[1], sort_keys=True) == g]
+                if n < 2 or not ms:
+                    continue
+                job = {"workload": a.workload, "frames": a.frames, "fpl": fpl, "tuning": json.loads(g), "stripes": n,
+                       "stripe_rows": a.stripe_rows, "share_ms_max": max(ms), "share_ms_mean": round(sum(ms) / len(ms), 3),
+                       "max_over_mean": round(max(ms) / (sum(ms) / len(ms)), 4),
+                       "job_Msamples_s": round(w * h * a.frames * depth / (max(ms) / 1e3) / 1e6, 1)}
+                print(json.dumps(job), flush=True)
+                out.append(job)
     if a.json:
         with open(a.json, "a") as fh:
             for r in out:
