@@ -264,6 +264,9 @@ def main():
     ap.add_argument("--tile-order", type=int, default=-1,
                     help="k_render queue tile order (mcpt_tuning.tile_order: 0 dearest first by the costliest "
                          "pixel, 1 image order, 2 by summed cost); -1: tuned with the block sizing")
+    ap.add_argument("--quantized", type=int, default=0, choices=[0, 1, 2],
+                    help="EXACT search-tree format (mcpt_tuning.quantized: 0 auto, 1 the 64-B quantized nodes, "
+                         "2 the 128-B nodes)")
     args = ap.parse_args()
     global W, H_PER_GPU, DEPTH
     wl = WORKLOADS[args.workload]
@@ -310,6 +313,8 @@ def main():
         rnd.set_tuning(**dict(rnd.get_tuning(), last_block_frames=args.last_block_frames))
     if args.tile_order >= 0:
         rnd.set_tuning(**dict(rnd.get_tuning(), tile_order=args.tile_order))
+    if args.quantized:
+        rnd.set_tuning(**dict(rnd.get_tuning(), quantized=args.quantized))
     shade_th = rnd.get_tuning()["shade_threshold"] or 32
     if args.schedule == "auto" and args.shade_threshold > 0:
         rnd.tune_schedule(dsc, cam, st, DEPTH, attempt, frames=max(1, min(args.steps, 64)), trials=3, **kw)

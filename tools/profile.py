@@ -82,6 +82,8 @@ def run(tag, args):
     if "tile_order" in cfg:
         quiet += ["--tile-order", str({"dearest first (costliest pixel)": 0, "image": 1,
                                        "dearest first (summed)": 2}[cfg["tile_order"]])]
+    if "--quantized" in args:  # the search-tree format the command forced
+        quiet += ["--quantized", args[args.index("--quantized") + 1]]
     sh(["rocprofv3", "--kernel-trace", "--stats", "--output-format", "csv", "-d", os.path.join(out, "trace"), "--"]
        + quiet, os.path.join(out, "trace.log"), 400)
     print("trace done", flush=True)
