@@ -70,6 +70,7 @@ def main():
     times = {i: [] for i in range(len(combos))}
     ticks = {}
     fpb = {}
+    prim = {}
     for i, (fpl, g, n, r) in enumerate(combos):  # warm every variant once
         rnd.set_tuning(**g)
         rnd.render_frames(dsc, cam, st, depth, 1 << 30, min(a.frames, 4), frames_per_launch=fpl, stripe_count=n, stripe_index=r, stripe_rows=a.stripe_rows)
@@ -92,6 +93,8 @@ def main():
                 rnd.render_frames(dsc, cam, st, depth, 1 << 30, a.frames, frames_per_launch=fpl, stripe_count=n, stripe_index=r, stripe_rows=a.stripe_rows)
                 s = rnd.stats()
                 times[i].append(s["kernel_ms"])
+                if s.get("primary_cache") == 2:  # this call ran the primary-hit pass (part of kernel_ms)
+                    prim.setdefault(i, []).append(s["primary_ms"])
             fpb[i] = s["frames_per_block"]
             if any(s["phase_ticks"]):  # an MCPT_PHASE_TIMING build (MCPT_LIB_OVERRIDE)
                 ticks.setdefault(i, [0, 0, 0, 0])
@@ -103,6 +106,9 @@ def main():
         rec = {"workload": a.workload, "frames": a.frames, "fpl": fpl, "fpb": fpb[i], "tuning": g,
                "kernel_ms_median": round(med, 3), "kernel_ms_min": round(ts[0], 3),
                "Msamples_s": round(w * h * a.frames * depth / (med / 1e3) / 1e6, 1)}
+        if i in prim:
+            ps = sorted(prim[i])
+            rec["primary_ms_median"] = round(ps[len(ps) // 2], 4)
         if a.calls > 1:
             rec.update({"calls": a.calls, "frames_per_call": per_call, "wall_ms_median": rec.pop("kernel_ms_median"),
                         "ms_per_frame": round(med / (a.calls * per_call), 4)})
