@@ -156,10 +156,11 @@ constexpr int64_t kQuantAutoBytes = 32ll << 20;  // 8 XCDs x 4 MiB of L2
 // size, k_render's PRIM form (batched phases, resident grid) beyond: C3's
 // 0.24 MB tree 0.07 vs 0.13 ms, C2's 2.1 MB 0.18 vs 0.15, C5's 435 MB 3.57 vs
 // 1.66 (profiles/r02_primary_cache.txt)
-constexpr int64_t kPrimSmallTree = 1ll << 20;     // k_render counters (mcpt_stats)
+constexpr int64_t kPrimSmallTree = 1ll << 20;
+// k_render counters (mcpt_stats): kStatSlots words
 constexpr int kPhaseSlot = 16;     // MCPT_PHASE_TIMING: shader-clock ticks per phase (fetch, T, L, S)
-constexpr int kDebugSlot = 12;
-constexpr int kWaveLogWords = 8;   // MCPT_PHASE_TIMING wave log (mcpt_get_wave_log)     // MCPT_DEBUG: violations of the stack bound, node and triangle indices
+constexpr int kDebugSlot = 12;     // MCPT_DEBUG: violations of the stack bound, node and triangle indices
+constexpr int kWaveLogWords = 8;   // MCPT_PHASE_TIMING wave log (mcpt_get_wave_log)
 
 // -DMCPT_DEBUG (make debug -> lib/libmcpt_hip_debug.so): k_render checks every
 // stack push against its capacity and every node / triangle index against
@@ -1020,7 +1021,7 @@ __global__ void __launch_bounds__(64, MCPT_WAVES_PER_SIMD) k_render(RenderArgs A
             const uint32_t items = queue_items(qx, n_tiles, nq);
             const uint32_t b = q / items, j = q - b * items;
             uint32_t u = j >> 6, kk = j & 63u;  // the queue's tile u, its pixel kk
-            if (!PRIM && A.spread) {
+            if (A.spread) {
               // spread: slot j of the group of (up to) 64 tiles g0.. is pixel
               // i / gs of tile g0 + i % gs, i = its index in the group, so a
               // wave's 64 consecutive slots come from 64 tiles and the dear
@@ -1838,7 +1839,7 @@ int mcpt_set_tuning(mcpt_ctx *c, const mcpt_tuning *t) {
             t->primary_cache < 0 || t->primary_cache > 2 || t->lds_pad < 0 || t->lds_pad > 65536 ||
             t->queue_chunk > 4096 || t->leaf_threshold > 64 || t->shade_threshold > 64 || t->fetch_threshold > 64 ||
             t->last_block_frames < -1 || t->tile_order < 0 || t->tile_order > 2 || t->pixel_spread < 0 ||
-            t->pixel_spread > 2))
+            t->pixel_spread > 6))
     return mcpt::fail(MCPT_ERR_ARG, "set_tuning: value out of range");
   if (t)
     c->tune = *t;
@@ -2536,6 +2537,7 @@ int mcpt_render_frames(mcpt_ctx *ctx, const mcpt_scene *scene, const mcpt_camera
   // 4 ranks: C2 6.51 -> 5.22, C4 76.7 -> 73.0; whole images even (C2, C3, C4,
   // C5 within 0.7 %; profiles/r04_spread.jsonl).
   A.spread = T.pixel_spread == 2 || (T.pixel_spread == 0 && px_per_lane <= 2.5) ? 1 : 0;
+  if (T.pixel_spread >= 3) A.spread = 0;  // EXPERIMENT
   A.entry_log = nullptr;
   ctx->entry_log_n = 0;
   if (kTiming && n_launch == 1 && (int64_t)p->width * p->height * n_blocks_all <= (16ll << 20)) {
@@ -2619,6 +2621,9 @@ int mcpt_render_frames(mcpt_ctx *ctx, const mcpt_scene *scene, const mcpt_camera
           Ap.px_segments = nullptr;
           Ap.px_iters = nullptr;
           Ap.entry_log = nullptr;
+          Ap.spread = (T.pixel_spread == 3 || T.pixel_spread == 5) ? 1 : 0;  // EXPERIMENT
+          if (T.pixel_spread == 4 || T.pixel_spread == 5) Ap.th_shade = 1;  // EXPERIMENT
+          if (T.pixel_spread == 6) Ap.th_shade = 1, Ap.th_leaf = 1;  // EXPERIMENT
           Ap.queue = ctx->d_queue + (size_t)n_launch * kQueues * kQueueStride;
           HIP_OK(hipMemsetAsync(Ap.queue, 0, (size_t)kQueues * kQueueStride * sizeof(uint32_t), st));
           // its own resident grid: the PRIM form needs fewer registers
