@@ -733,3 +733,30 @@ def test_integration_snippet_matches_abi_host():
     want = calls(body) + ["mcpt_write_hdr"]
     assert calls(snippet) == want
     assert "mcpt_treelet_gpu" in want
+
+
+def _spread_slot(j, items):
+    """mcpt_device.hip k_render fetch, pixel_spread on: queue slot j of a queue
+    holding items / 64 tiles -> (the queue's tile u, its pixel k)."""
+    u, k = j >> 6, j & 63
+    g0 = u & ~63
+    gs = min(64, (items >> 6) - g0)
+    i = ((u - g0) << 6) + k
+    return g0 + i % gs, i // gs
+
+
+@pytest.mark.parametrize("n_tiles", [1, 7, 64, 65, 130, 1000, 16384])
+def test_spread_slot_mapping_is_a_bijection(n_tiles):
+    """The spread slot mapping (mcpt_tuning.pixel_spread) restated: on every
+    queue (tiles x, x + nq, ...; queue_items slots) it is a bijection of the
+    queue's slots onto its (tile, pixel) pairs -- partial last groups
+    included -- and a run of 64 consecutive slots of a full group takes one
+    pixel of each of 64 tiles."""
+    for nq in (1, 3, 8):
+        for x in range(nq):
+            n_q = (n_tiles - 1 - x) // nq + 1 if x < n_tiles else 0
+            items = n_q * 64
+            got = [_spread_slot(j, items) for j in range(items)]
+            assert sorted(got) == [(u, k) for u in range(n_q) for k in range(64)]
+            if n_q >= 64:
+                assert len({u for u, _ in got[:64]}) == 64
