@@ -340,6 +340,27 @@ def main():
                      "ms_per_step": round(e_off * 1e3 / args.steps, 4),
                      "note": "mcpt_tuning.primary_cache = 2: every frame traces its primary ray (same bits)"}
         del st_off
+    # the boundary keeps the image state in HBM across calls (the reference's
+    # OpenCL buffers live on its device too); host copies happen only at a
+    # dump (ColorOut): this rank's hist/count/seeds to pinned host memory,
+    # timed apart from value (PCIe-inclusive rate)
+    dump = None
+    if rank == 0:
+        host = [torch.empty(t.shape, dtype=t.dtype, pin_memory=True) for t in (st.hist, st.count, st.seeds)]
+        ts = []
+        for _ in range(3):
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for hbuf, t in zip(host, (st.hist, st.count, st.seeds)):
+                hbuf.copy_(t, non_blocking=True)
+            torch.cuda.synchronize()
+            ts.append(time.perf_counter() - t0)
+        dump_s = sorted(ts)[1]
+        nbytes = sum(t.numel() * t.element_size() for t in (st.hist, st.count, st.seeds))
+        dump = {"ms": round(dump_s * 1e3, 3), "bytes": nbytes, "GBps": round(nbytes / dump_s / 1e9, 1),
+                "value_with_dump_per_call": round(float(W * h_img) * args.steps * DEPTH / (elapsed + dump_s) / 1e6, 2),
+                "note": "device-to-host copy of the image state (24 B/pixel) after the call, outside value"}
+        del host
     # k_render alone: the call's device time less the primary-hit pass before it
     primary_ms = kst.get("primary_ms", 0.0) if kst.get("primary_cache") == 2 else 0.0
     kernel_ms, launches = kst["kernel_ms"] - primary_ms, max(kst["launches"], 1)
@@ -491,6 +512,7 @@ def main():
                "traced_Msegments_per_s": round(traced * n / elapsed / 1e6, 2),
                "primary_cache_off": cache_off,
                "image_reduce_ms": None if reduce_ms is None else round(reduce_ms, 3),
+               "host_dump": dump,
                "strong_scaling": strong,
                "roofline": roof, "cpu_baseline": cpu}
         print(json.dumps(out), flush=True)

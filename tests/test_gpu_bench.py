@@ -47,6 +47,8 @@ def test_bench_two_ranks_rehearsal():
     assert j["strong_scaling"]["value"] > 0 and j["strong_scaling"]["image"] == [1024, 1024]
     assert j["cpu_baseline"] is None  # rank 0 at N=1 only
     assert j["image_reduce_ms"] is not None and j["image_reduce_ms"] > 0  # the final image reduce ran
+    # the host dump (device-to-host copy of rank 0's image state), timed outside value
+    assert j["host_dump"]["bytes"] == 1024 * 2048 * 24 and j["host_dump"]["value_with_dump_per_call"] < j["value"]
 
 
 def test_bench_c4_strong_two_ranks_rehearsal():
