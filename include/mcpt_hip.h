@@ -233,10 +233,6 @@ typedef struct mcpt_tuning {
                                consecutive slots are one 8x8 tile), 2 spread
                                (they are one pixel of each of 64 tiles, so one
                                tile's dear pixels run in different waves)      */
-  int32_t node_threshold;   /* lanes in a node step before the T phase runs
-                               while the L or S phase has its lanes, for 64
-                               live lanes (0: the T phase runs every loop
-                               iteration that has a lane in it)                */
 } mcpt_tuning;
 
 /* ------------------------------------------------------- version / errors */

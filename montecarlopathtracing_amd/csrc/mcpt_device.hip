@@ -780,7 +780,6 @@ struct RenderArgs {
   uint32_t tag_base;           // this launch's tag; a granule for block b carries tag_base | b (16 bits)
   int32_t stack_depth;
   int32_t th_leaf, th_shade;  // lanes waiting before the L / S phase runs
-  int32_t th_node;            // lanes in T before the T phase runs while another phase can run (0: always)
   uint32_t *queue;            // n_queues work-queue heads, kQueueStride apart (zeroed before each launch)
   uint32_t n_queues;          // 1..kQueues
   int32_t lds_mats;           // 1: copy the material table to LDS after the stack
@@ -1111,20 +1110,7 @@ __global__ void __launch_bounds__(64, MCPT_WAVES_PER_SIMD) k_render(RenderArgs A
     }
     // ---- T: one node step (objdef.h:252-273 with child boxes)
     const bool in_t = live && cur >= 0;
-    const unsigned long long mt = __ballot(in_t);
-    bool run_t = mt != 0;
-    if (A.th_node > 0 && run_t) {
-      // node threshold: with fewer T lanes than th_node (scaled to the live
-      // lanes), the T phase waits while the L or S phase has its lanes, so a
-      // node step's gathers serve more lanes; nothing else to run: it runs
-      const int n_t = __popcll(mt), th_node = max(1, (A.th_node * n_live + 63) >> 6);
-      if (n_t < th_node) {
-        const int n_l = __popcll(__ballot(live && cur < 0 && cur != kDone));
-        const int n_s = __popcll(__ballot(live && cur == kDone));
-        run_t = !(n_l >= th_leaf || n_s >= th_shade);
-      }
-    }
-    if (run_t) {
+    if (__ballot(in_t)) {
       if (STATS && lane == __builtin_ctzll(__ballot(1))) w_t++;
       if (in_t) {
         if (Q) {  // EXACT, quantized SAH tree nearest-first (4 loads), or the reference tree left-first
@@ -1853,7 +1839,7 @@ int mcpt_set_tuning(mcpt_ctx *c, const mcpt_tuning *t) {
             t->primary_cache < 0 || t->primary_cache > 2 || t->lds_pad < 0 || t->lds_pad > 65536 ||
             t->queue_chunk > 4096 || t->leaf_threshold > 64 || t->shade_threshold > 64 || t->fetch_threshold > 64 ||
             t->last_block_frames < -1 || t->tile_order < 0 || t->tile_order > 2 || t->pixel_spread < 0 ||
-            t->pixel_spread > 2 || t->node_threshold > 64))
+            t->pixel_spread > 2))
     return mcpt::fail(MCPT_ERR_ARG, "set_tuning: value out of range");
   if (t)
     c->tune = *t;
@@ -2349,7 +2335,6 @@ int mcpt_render_frames(mcpt_ctx *ctx, const mcpt_scene *scene, const mcpt_camera
   A.th_shade = T.shade_threshold > 0 ? T.shade_threshold : 32;
   A.chunk = T.queue_chunk > 0 ? T.queue_chunk : 4;  // queue entries per atomic (at least)
   A.th_fetch = T.fetch_threshold > 0 ? T.fetch_threshold : 1;
-  A.th_node = T.node_threshold > 0 ? T.node_threshold : 0;
   A.n_queues = T.queues > 0 ? (uint32_t)std::min(T.queues, kQueues) : (uint32_t)kQueues;
   const int64_t tiles = (int64_t)A.tiles_x * ((A.local_rows + 7) / 8);
   const int depth_entries = p->mode == MCPT_MODE_NOPRUNE ? scene->stack_depth : scene->stack_depth4;

@@ -412,8 +412,7 @@ def test_launch_knobs_change_no_bits_full_size(rnd):
                 {"queues": 1}, {"queues": 3, "fetch_threshold": 5}, {"primary_cache": 2}, {"primary_cache": 1},
                 {"tile_order": 1}, {"tile_order": 2}, {"tile_order": 2, "queues": 3}, {"pixel_spread": 2},
                 {"pixel_spread": 2, "queues": 3, "block_entries": 4, "max_block_frames": 2},
-                {"pixel_spread": 2, "tile_order": 1, "queues": 5}, {"node_threshold": 16},
-                {"node_threshold": 48, "pixel_spread": 2}]
+                {"pixel_spread": 2, "tile_order": 1, "queues": 5}]
     outs = []
     try:
         for t in settings:
