@@ -39,12 +39,15 @@ def summarize(log, ms):
     ts = np.linspace(first_dry, end.max(), 64)
     alive = [(end > t).mean() for t in ts]
     slow = np.argsort(end)[-16:]  # the 16 last workgroups
+    ts_all = np.linspace(t0, end.max(), 128)
+    alive_all = [((st <= t) & (end > t)).mean() for t in ts_all]
     return {"kernel_ms": round(ms, 3), "span_us": round(float(span), 1),
             "start_spread_us": round(float(us(st.max())), 1),
             "first_dry_us": round(float(us(first_dry)), 1),
             "tail_us_p50_p90_max": [round(float(np.percentile(tail, q)), 1) for q in (50, 90, 100)],
             "tail_share_of_span": round(float((end.max() - first_dry) / 100.0 / span), 4),
             "alive_mean_over_tail": round(float(np.mean(alive)), 4),
+            "alive_mean_over_span": round(float(np.mean(alive_all)), 4),
             "last_start_after_dry_us_p50_max": [round(float(np.percentile((last - first_dry) / 100.0, 50)), 1),
                                                 round(float(((last - first_dry) / 100.0).max()), 1)],
             "slowest16_last_start_after_dry_us": [round(float(x), 1) for x in (last[slow] - first_dry) / 100.0],
@@ -63,6 +66,7 @@ def entry_summary(el, log):
     to the first queue-dry moment of the wave log: how long entries waited
     for their pixel's previous block, how long they ran, and the chains of
     the pixels that ended last."""
+    el = el[(el[:, :, 2] != 0).all(axis=1)]  # pixels this call rendered (a share leaves the others at 0)
     dry32 = np.uint32(int(log[:, 1].min()) & 0xFFFFFFFF)
     rel = ((el.astype(np.int64) - int(dry32) + (1 << 31)) % (1 << 32) - (1 << 31)) / 100.0  # us from first dry
     claim, start, end = rel[..., 0], rel[..., 1], rel[..., 2]
@@ -91,7 +95,10 @@ def main():
     ap.add_argument("--fpl", default="0")
     ap.add_argument("--tuning", default="shade_threshold=32,fetch_threshold=8,block_entries=16")
     ap.add_argument("--out", default=os.path.join(ROOT, "gpurun_out", "tail_probe.jsonl"))
+    ap.add_argument("--stripes", type=int, default=1, help="render one rank's share: 16-row stripes dealt to this many ranks")
+    ap.add_argument("--stripe-index", type=int, default=0)
     a = ap.parse_args()
+    kw = dict(stripe_count=a.stripes, stripe_index=a.stripe_index)
     wl = bench.WORKLOADS[a.workload]
     data, camj = bench.load_scene(a.workload)
     cam = S.parse_camera(camj)
@@ -104,15 +111,16 @@ def main():
     with open(a.out, "a") as fh:
         for fpl in (int(x) for x in a.fpl.split(",")):
             st = rnd.new_state(wl["w"], wl["h"])
-            rnd.render_frames(dsc, cam, st, wl["depth"], 1 << 30, 4, frames_per_launch=fpl)  # warm
+            rnd.render_frames(dsc, cam, st, wl["depth"], 1 << 30, 4, frames_per_launch=fpl, **kw)  # warm
             for rep in range(3):
                 rnd.drop_caches()
-                rnd.render_frames(dsc, cam, st, wl["depth"], 1 << 30, a.frames, frames_per_launch=fpl)
+                rnd.render_frames(dsc, cam, st, wl["depth"], 1 << 30, a.frames, frames_per_launch=fpl, **kw)
                 s = rnd.stats()
                 log = rnd.wave_log()
                 if len(log) == 0:
                     raise SystemExit("no wave log: run with the MCPT_PHASE_TIMING library (MCPT_LIB_OVERRIDE)")
                 rec = dict(workload=a.workload, frames=a.frames, fpl=fpl, frames_per_block=s["frames_per_block"],
+                           stripes=a.stripes, stripe_index=a.stripe_index,
                            rep=rep, primary_ms=round(s.get("primary_ms", 0.0), 3), **summarize(log, s["kernel_ms"]))
                 print(json.dumps(rec), flush=True)
                 if rep == 0:
