@@ -33,11 +33,11 @@ def child(a):
     if a.tuning:
         rnd.set_tuning(**{k: int(v) for k, v in (x.split("=") for x in a.tuning.split(","))})
     st = rnd.new_state(wl["w"], wl["h"])
-    rnd.render_frames(dsc, cam, st, wl["depth"], 1 << 30, 4, frames_per_launch=a.fpl, stripe_count=a.stripes)
+    rnd.render_frames(dsc, cam, st, wl["depth"], 1 << 30, 4, frames_per_launch=a.fpl, stripe_count=a.stripes, stripe_index=a.stripe_index)
     ms = []
     for _ in range(a.reps):
         rnd.render_frames(dsc, cam, st, wl["depth"], 1 << 30, a.frames, frames_per_launch=a.fpl,
-                          stripe_count=a.stripes)
+                          stripe_count=a.stripes, stripe_index=a.stripe_index)
         ms.append(rnd.stats()["kernel_ms"])
     print("AB_RESULT " + json.dumps(ms), flush=True)
 
@@ -53,6 +53,7 @@ def main():
     ap.add_argument("--schedule", default="paired", choices=["single", "paired"])
     ap.add_argument("--tuning", default="", help="set_tuning knobs for every library, e.g. shade_threshold=40,fetch_threshold=8")
     ap.add_argument("--stripes", type=int, default=1, help="rank 0's share of an N-rank strong-scaled job")
+    ap.add_argument("--stripe-index", type=int, default=0, help="with --stripes: this rank's share")
     ap.add_argument("--child", action="store_true")
     a = ap.parse_args()
     if a.child:
@@ -65,7 +66,8 @@ def main():
             out = subprocess.run([sys.executable, os.path.abspath(__file__), "--child", "--libs", lib,
                                   "--workload", a.workload, "--frames", str(a.frames), "--fpl", str(a.fpl),
                                   "--schedule", a.schedule, "--tuning", a.tuning,
-                                  "--reps", str(a.reps), "--stripes", str(a.stripes)], env=env, capture_output=True, text=True, timeout=600)
+                                  "--reps", str(a.reps), "--stripes", str(a.stripes), "--stripe-index", str(a.stripe_index)],
+                                 env=env, capture_output=True, text=True, timeout=600)
             line = [x for x in out.stdout.splitlines() if x.startswith("AB_RESULT ")]
             if out.returncode != 0 or not line:
                 print(out.stdout[-2000:], out.stderr[-2000:])
@@ -76,7 +78,7 @@ def main():
     for lib in libs:
         ts = sorted(res[lib])
         print(json.dumps({"lib": os.path.basename(lib), "workload": a.workload, "frames": a.frames, "fpl": a.fpl,
-                          "stripes": a.stripes,
+                          "stripes": a.stripes, "stripe_index": a.stripe_index,
                           "schedule": a.schedule,
                           "kernel_ms_median": round(ts[len(ts) // 2], 3), "kernel_ms_min": round(ts[0], 3),
                           "n": len(ts)}), flush=True)
