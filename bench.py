@@ -317,11 +317,11 @@ def main():
         rnd.set_tuning(**dict(rnd.get_tuning(), quantized=args.quantized))
     shade_th = rnd.get_tuning()["shade_threshold"] or 32
     if args.schedule == "auto" and args.shade_threshold > 0:
-        rnd.tune_schedule(dsc, cam, st, DEPTH, attempt, frames=max(1, min(args.steps, 64)), trials=3, **kw)
+        rnd.tune_schedule(dsc, cam, st, DEPTH, attempt, frames=max(1, min(args.steps, 64)), trials=5, **kw)
     elif args.schedule == "auto":
         # timed on calls of the timed call's size (same frame-block regime), 3 trials each
         # and the S-phase threshold (speed only; every setting gives the same bits)
-        _, shade_th, _ = rnd.tune(dsc, cam, st, DEPTH, attempt, frames=max(1, min(args.steps, 64)), trials=3, **kw)
+        _, shade_th, _ = rnd.tune(dsc, cam, st, DEPTH, attempt, frames=max(1, min(args.steps, 64)), trials=5, **kw)
     else:
         dsc.schedule = L.SCHED_PAIRED if args.schedule == "paired" else L.SCHED_SINGLE
 
