@@ -280,16 +280,18 @@ class Renderer:
         differ by scene (round 2, 3-frame blocks: veach_mis S 40, fetch 8;
         cbox S 32-40, fetch 8; the 10 M-triangle soup S 32, fetch 1; round 4:
         cbox gains 5-10 % from the dearest-first order, veach_mis loses 5 %).
-        Every combination gives the same bits.  The winner goes to
+        Every combination gives the same bits.  Each setting is judged by its
+        median over the trials (a single timed call is what the pick has to
+        predict; the minimum favoured lucky runs).  The winner goes to
         scene.schedule and the renderer's tuning.  Returns (schedule,
-        shade_threshold, {(schedule, shade, fetch, entries, tile_order): best ms})."""
+        shade_threshold, {(schedule, shade, fetch, entries, tile_order): median ms})."""
         if getattr(self, "_stats_on", False):
             raise L.MCPTError("tune: counters must be off (they change the kernel)")
         base = self.get_tuning()
         ths = list(shade_thresholds) if shade_thresholds else [base["shade_threshold"]]
         scratch = ImageState.__new__(ImageState)
         scratch.width, scratch.height, scratch.frames_done = state.width, state.height, state.frames_done
-        best = {}
+        best, samples = {}, {}
 
         def trial(sched, th, fe, be, to):
             self.set_tuning(**dict(base, shade_threshold=th, fetch_threshold=fe, block_entries=be, tile_order=to))
@@ -297,10 +299,11 @@ class Renderer:
             self.render_frames(scene, camera, scratch, max_depth, max_attempt, frames,
                                frame_begin=state.frames_done, schedule=sched, **kw)
             ms = self.stats()["kernel_ms"]
-            key = (sched, th, fe, be, to)
-            best[key] = min(best.get(key, ms), ms)
+            samples.setdefault((sched, th, fe, be, to), []).append(ms)
+            best.clear()  # median per setting: a single timed call is what the pick predicts
+            best.update({k: sorted(v)[len(v) // 2] for k, v in samples.items()})
 
-        def pick():  # fastest; ties to the smaller key
+        def pick():  # fastest median; ties to the smaller key
             return min(best, key=lambda k: (best[k], k))
 
         fe0 = base["fetch_threshold"] or 1  # 0 = the default, 1
@@ -337,7 +340,7 @@ class Renderer:
             if shade_thresholds and last_block:  # then a short last block against equal blocks
                 lbs = {-1, (int(frames) + 7) // 8}
                 key = (sched, th, fe, be, to)
-                lbest = {lb: best[key]}
+                lsamples = {lb: list(samples[key])}
                 for _ in range(int(trials)):
                     for v in sorted(lbs - {lb}):
                         self.set_tuning(**dict(base, shade_threshold=th, fetch_threshold=fe, block_entries=be,
@@ -346,8 +349,8 @@ class Renderer:
                                                                       state.count.clone())
                         self.render_frames(scene, camera, scratch, max_depth, max_attempt, frames,
                                            frame_begin=state.frames_done, schedule=sched, **kw)
-                        ms = self.stats()["kernel_ms"]
-                        lbest[v] = min(lbest.get(v, ms), ms)
+                        lsamples.setdefault(v, []).append(self.stats()["kernel_ms"])
+                lbest = {k: sorted(v)[len(v) // 2] for k, v in lsamples.items()}
                 # ties go to the baseline (the auto rule's value), then to the smaller key
                 lb = min(lbest, key=lambda k: (lbest[k], k != base["last_block_frames"], k))
         finally:
