@@ -321,7 +321,9 @@ def main():
     elif args.schedule == "auto":
         # timed on calls of the timed call's size (same frame-block regime), 3 trials each
         # and the S-phase threshold (speed only; every setting gives the same bits)
-        _, shade_th, _ = rnd.tune(dsc, cam, st, DEPTH, attempt, frames=max(1, min(args.steps, 64)), trials=5, **kw)
+        # each trial as the timed call runs: a fresh view (primary-hit pass and tile sort included)
+        _, shade_th, _ = rnd.tune(dsc, cam, st, DEPTH, attempt, frames=max(1, min(args.steps, 64)), trials=5,
+                                  fresh_view=True, **kw)
     else:
         dsc.schedule = L.SCHED_PAIRED if args.schedule == "paired" else L.SCHED_SINGLE
 

@@ -268,7 +268,8 @@ class Renderer:
         return sched, {k[0]: v for k, v in best.items()}
 
     def tune(self, scene, camera, state, max_depth, max_attempt, frames=64, trials=1, shade_thresholds=(32, 40, 48),
-             fetch_thresholds=(1, 8), block_entries=(8, 16), last_block=True, tile_orders=(0, 1, 2), **kw):
+             fetch_thresholds=(1, 8), block_entries=(8, 16), last_block=True, tile_orders=(0, 1, 2), fresh_view=False,
+             **kw):
         """tune_schedule over the leaf-test schedule, the S-phase threshold
         (mcpt_tuning.shade_threshold) and then the fetch threshold
         (mcpt_tuning.fetch_threshold), then the block sizing
@@ -282,7 +283,10 @@ class Renderer:
         cbox gains 5-10 % from the dearest-first order, veach_mis loses 5 %).
         Every combination gives the same bits.  Each setting is judged by its
         median over the trials (a single timed call is what the pick has to
-        predict; the minimum favoured lucky runs).  The winner goes to
+        predict; the minimum favoured lucky runs).  fresh_view: every trial
+        call first drops the primary-hit cache, so it pays the primary-hit
+        pass and the tile sort as a call of a new view does (bench.py's timed
+        call).  The winner goes to
         scene.schedule and the renderer's tuning.  Returns (schedule,
         shade_threshold, {(schedule, shade, fetch, entries, tile_order): median ms})."""
         if getattr(self, "_stats_on", False):
@@ -296,6 +300,8 @@ class Renderer:
         def trial(sched, th, fe, be, to):
             self.set_tuning(**dict(base, shade_threshold=th, fetch_threshold=fe, block_entries=be, tile_order=to))
             scratch.seeds, scratch.hist, scratch.count = state.seeds.clone(), state.hist.clone(), state.count.clone()
+            if fresh_view:
+                self.drop_caches()
             self.render_frames(scene, camera, scratch, max_depth, max_attempt, frames,
                                frame_begin=state.frames_done, schedule=sched, **kw)
             ms = self.stats()["kernel_ms"]
@@ -347,6 +353,8 @@ class Renderer:
                                                tile_order=to, last_block_frames=v))
                         scratch.seeds, scratch.hist, scratch.count = (state.seeds.clone(), state.hist.clone(),
                                                                       state.count.clone())
+                        if fresh_view:
+                            self.drop_caches()
                         self.render_frames(scene, camera, scratch, max_depth, max_attempt, frames,
                                            frame_begin=state.frames_done, schedule=sched, **kw)
                         lsamples.setdefault(v, []).append(self.stats()["kernel_ms"])
