@@ -276,8 +276,8 @@ class Renderer:
         (mcpt_tuning.block_entries) jointly with the tile order
         (mcpt_tuning.tile_order: dearest tiles first by their costliest or
         summed primary-ray cost, or image order), then a short last block
-        against equal blocks (mcpt_tuning.last_block_frames -1 or
-        ceil(frames / 8)); ties keep the baseline value.  Their best values
+        against equal blocks (mcpt_tuning.last_block_frames -1, ceil(frames / 8)
+        or ceil(frames / 4)); ties keep the baseline value.  Their best values
         differ by scene (round 2, 3-frame blocks: veach_mis S 40, fetch 8;
         cbox S 32-40, fetch 8; the 10 M-triangle soup S 32, fetch 1; round 4:
         cbox gains 5-10 % from the dearest-first order, veach_mis loses 5 %).
@@ -344,7 +344,7 @@ class Renderer:
                     sched, th, fe, be, to = pick()
             lb = base["last_block_frames"]
             if shade_thresholds and last_block:  # then a short last block against equal blocks
-                lbs = {-1, (int(frames) + 7) // 8}
+                lbs = {-1, (int(frames) + 7) // 8, (int(frames) + 3) // 4}  # C2, 20 frames: 5 beats 3 by 2.5 %
                 key = (sched, th, fe, be, to)
                 lsamples = {lb: list(samples[key])}
                 for _ in range(int(trials)):
