@@ -277,7 +277,8 @@ class Renderer:
         (mcpt_tuning.tile_order: dearest tiles first by their costliest or
         summed primary-ray cost, or image order), then a short last block
         against equal blocks (mcpt_tuning.last_block_frames -1, ceil(frames / 8)
-        or ceil(frames / 4)); ties keep the baseline value.  Their best values
+        or ceil(frames / 4)) jointly with the block sizing again; ties keep the
+        baseline value.  Their best values
         differ by scene (round 2, 3-frame blocks: veach_mis S 40, fetch 8;
         cbox S 32-40, fetch 8; the 10 M-triangle soup S 32, fetch 1; round 4:
         cbox gains 5-10 % from the dearest-first order, veach_mis loses 5 %).
@@ -343,24 +344,31 @@ class Renderer:
                                 trial(sched, t, fe, be, to)
                     sched, th, fe, be, to = pick()
             lb = base["last_block_frames"]
-            if shade_thresholds and last_block:  # then a short last block against equal blocks
-                lbs = {-1, (int(frames) + 7) // 8, (int(frames) + 3) // 4}  # C2, 20 frames: 5 beats 3 by 2.5 %
-                key = (sched, th, fe, be, to)
-                lsamples = {lb: list(samples[key])}
+            if shade_thresholds and last_block:
+                # then a short last block against equal blocks, jointly with the
+                # block sizing: the best last block can belong to the sizing
+                # that lost with equal blocks (C2, 20 frames: (15, 5) at 8
+                # entries beats 5-frame blocks at 16, which beat (10, 10))
+                lbs = {-1, (int(frames) + 7) // 8, (int(frames) + 3) // 4}
+                bes = sorted(set(block_entries)) if block_entries else [be]
+                lsamples = {(be, lb): list(samples[(sched, th, fe, be, to)])}
                 for _ in range(int(trials)):
-                    for v in sorted(lbs - {lb}):
-                        self.set_tuning(**dict(base, shade_threshold=th, fetch_threshold=fe, block_entries=be,
-                                               tile_order=to, last_block_frames=v))
-                        scratch.seeds, scratch.hist, scratch.count = (state.seeds.clone(), state.hist.clone(),
-                                                                      state.count.clone())
-                        if fresh_view:
-                            self.drop_caches()
-                        self.render_frames(scene, camera, scratch, max_depth, max_attempt, frames,
-                                           frame_begin=state.frames_done, schedule=sched, **kw)
-                        lsamples.setdefault(v, []).append(self.stats()["kernel_ms"])
+                    for b in bes:
+                        for v in sorted(lbs | {lb}):
+                            if (b, v) == (be, lb):
+                                continue
+                            self.set_tuning(**dict(base, shade_threshold=th, fetch_threshold=fe, block_entries=b,
+                                                   tile_order=to, last_block_frames=v))
+                            scratch.seeds, scratch.hist, scratch.count = (state.seeds.clone(), state.hist.clone(),
+                                                                          state.count.clone())
+                            if fresh_view:
+                                self.drop_caches()
+                            self.render_frames(scene, camera, scratch, max_depth, max_attempt, frames,
+                                               frame_begin=state.frames_done, schedule=sched, **kw)
+                            lsamples.setdefault((b, v), []).append(self.stats()["kernel_ms"])
                 lbest = {k: sorted(v)[len(v) // 2] for k, v in lsamples.items()}
-                # ties go to the baseline (the auto rule's value), then to the smaller key
-                lb = min(lbest, key=lambda k: (lbest[k], k != base["last_block_frames"], k))
+                # ties go to the baseline (the sizing picked above with the auto rule's value), then the smaller key
+                be, lb = min(lbest, key=lambda k: (lbest[k], k != (be, base["last_block_frames"]), k))
         finally:
             self.set_tuning(**base)
         scene.schedule = sched
