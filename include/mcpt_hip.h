@@ -216,9 +216,10 @@ typedef struct mcpt_tuning {
                                or more blocks: the last block of every pixel
                                is this many frames and the others share the
                                rest evenly (a short last block shortens the
-                               launch's tail); 0 auto (ceil(frames / 8) once
-                               there are >= 6 pixels per resident lane, else
-                               equal blocks), -1 equal blocks                 */
+                               launch's tail); 0 auto (ceil(frames / 8) from
+                               6 pixels per resident lane, ceil(frames / 4)
+                               from 2.5 on a whole image (stripe_count 1),
+                               else equal blocks), -1 equal blocks            */
   int32_t tile_order;       /* order of the 8x8 pixel tiles in the work queues:
                                0 auto (the primary-hit pass measures each
                                pixel's primary-ray traversal; tiles whose

@@ -2471,16 +2471,21 @@ int mcpt_render_frames(mcpt_ctx *ctx, const mcpt_scene *scene, const mcpt_camera
   // last block's entries are the launch's tail; shorter ones leave lanes idle
   // for less time at its end.  Same blocks, same hand-offs, same bits.
   // Auto: ceil(frames / 8) frames once a lane has at least 6 pixels (20-frame
-  // C3 -2 %, 16-frame C4 -2 %, 8-frame C5 -3 %); with fewer, the long head
-  // blocks' own chains end late (C2, 4 pixels per lane: +2-5 %), so auto
-  // leaves equal blocks there and Renderer.tune tries both.
+  // C3 -2 %, 16-frame C4 -2 %, 8-frame C5 -3 %); between 2.5 and 6 a longer
+  // one, ceil(frames / 4) (below); Renderer.tune tries equal blocks and both.
   int fpl_head = fpl;
   A.nb_head = INT32_MAX;  // every block fpl frames
   A.fpl_tail = fpl;
-  const bool tail_auto = T.last_block_frames == 0 && slots_per_px >= 6.0;
+  // Auto: ceil(frames / 8) from 6 pixels per lane; from 2.5, on a whole image (one
+  // stripe set), ceil(frames / 4): C2 and C3 at 4 pixels per lane, 20 frames: 9.00 /
+  // 2.98 ms against equal blocks' 9.34 / 3.08 (and (17, 3) 9.24 / 3.02); a strong-scaled
+  // share keeps equal blocks (the C5 4-rank share: 43.1 ms with (15, 5), 40.4 equal;
+  // profiles/r04_last_block_auto.jsonl)
+  const bool tail_auto = T.last_block_frames == 0 && (slots_per_px >= 6.0 || p->stripe_count == 1);
   if (tail_ok && n_launch == 1 && n_blocks_all >= 2 && (T.last_block_frames > 0 || tail_auto)) {
     const int nb = (int)n_blocks_all;
-    const int L = T.last_block_frames > 0 ? T.last_block_frames : (p->frames + 7) / 8;
+    const int L = T.last_block_frames > 0 ? T.last_block_frames
+                                          : (slots_per_px >= 6.0 ? (p->frames + 7) / 8 : (p->frames + 3) / 4);
     if (L < fpl) {
       const int head = (p->frames - L + nb - 2) / (nb - 1);
       const int last = p->frames - (nb - 1) * head;

@@ -492,7 +492,8 @@ def test_short_last_block_same_bits(rnd, diffuse):
         for attempt in (1 << 20, 18):
             outs, fpbs = [], []
             for t, fpl in (({}, 20), ({"last_block_frames": -1}, 0), ({"last_block_frames": 2}, 0),
-                           ({"last_block_frames": 3, "block_entries": 12}, 0), ({"last_block_frames": 9}, 0)):
+                           ({"last_block_frames": 3, "block_entries": 12}, 0), ({"last_block_frames": 9}, 0),
+                           ({}, 0)):
                 rnd.set_tuning(**t)
                 st = rnd.new_state(w, h, seeds)
                 rnd.render_frames(dsc, cam, st, 8, attempt, 20, frames_per_launch=fpl)
@@ -500,6 +501,7 @@ def test_short_last_block_same_bits(rnd, diffuse):
                 fpbs.append(rnd.stats()["frames_per_block"])
                 outs.append((st.hist.cpu().numpy(), st.count.cpu().numpy(), st.seeds_np()))
             assert fpbs[0] == 20 and fpbs[2] == 18, fpbs  # (18, 2): the short last block did run
+            assert fpbs[5] == 15, fpbs  # auto at 4 pixels per lane: (15, 5), a last block of ceil(20 / 4)
             for o in outs[1:]:
                 for a, b, what in zip(outs[0], o, ("hist", "count", "seeds")):
                     assert_bits_equal(a, b, what)
