@@ -1474,7 +1474,7 @@ __global__ void __launch_bounds__(64) k_primary(RenderArgs A, PrimHit *out) {
 
 // The dearest-first tile order (mcpt_tuning.tile_order): each 8x8 tile of
 // the rank's rows keyed by its pixels' primary-ray traversal cost (the
-// costliest pixel, or the sum), sorted descending (hipcub), so the tiles
+// costliest pixel, or the sum), counting-sorted descending (k_tile_sort), so the tiles
 // whose pixel chains take longest are claimed first.  Speed only: which lane
 // runs which entry when never changes a bit.
 constexpr int kTileBuckets = 256;  // tile-order keys: the cost saturated to 8 bits
