@@ -63,15 +63,34 @@ struct __attribute__((aligned(16))) DevNode {
   int32_t left, right, pad0, pad1;  // >= 0 internal node, < 0 leaf: ~triangle
 };
 // Cramer-ready triangle: v0, -(v1-v0), -(v2-v0) exactly as objdef.h:190-199
-// forms them, plus the packed normal (.w = material id bits).  The .w lanes
-// of v0/nab/nac carry the three triangle-only minors of cramer_reduced.
+// forms them, with the packed normal's xyz in their .w lanes, so a triangle
+// test reads the first 48 B: three gathers (the triangle-only minors of
+// cramer_reduced are recomputed from nab/nac, the same fma the host used,
+// tri_minors).  aux = the material id bits (the packed normal's .w), read once
+// per segment for the hit triangle, and the three minors (the quantized
+// records copy them).
 struct __attribute__((aligned(16))) DevTri {
-  f4 v0;   // .w = m_x1
-  f4 nab;  // .w = m_y4
-  f4 nac;  // .w = m_y8
-  f4 nrm;  // .w = material id bits
+  f4 v0;   // .w = normal.x
+  f4 nab;  // .w = normal.y
+  f4 nac;  // .w = normal.z
+  f4 aux;  // .x = material id bits, .yzw = m_x1, m_y4, m_y8
 };
 static_assert(sizeof(DevNode) == 64 && sizeof(DevTri) == 64, "64-B records");
+__host__ __device__ inline f3 tri_normal(const f4 &v0, const f4 &nab, const f4 &nac) {
+  return (f3){v0.w, nab.w, nac.w};
+}
+// the three triangle-only minors of cramer_reduced (mcpt_refmath.h): m_x1 =
+// fma(b2,c3,-(c2*b3)), m_y4 = fma(b1,c3,-(c1*b3)), m_y8 = fma(b1,c2,-(c1*b2))
+__device__ inline void tri_minors(f3 b, f3 c, float &m_x1, float &m_y4, float &m_y8) {
+  m_x1 = __builtin_fmaf(b.y, c.z, -(c.y * b.z));
+  m_y4 = __builtin_fmaf(b.x, c.z, -(c.x * b.z));
+  m_y8 = __builtin_fmaf(b.x, c.y, -(c.x * b.y));
+}
+// a traced hit carries its triangle as ~index in best_nrm.w (the material is
+// read at shading); a cached primary hit (PrimHit) carries the material id
+__device__ inline int32_t hit_material(const DevTri *__restrict__ tris, int32_t w) {
+  return w >= 0 ? w : as_i(tris[~w].aux.x);
+}
 
 // 4-wide node of the EXACT path: the binary HLBVH with every other level
 // collapsed.  Slots are the node's grandchildren (or a child that is a leaf)
@@ -456,7 +475,7 @@ __device__ inline Trace traverse_noprune(const SceneView &S, f3 o, f3 d, float t
     if (cur != kDone) {
       const int32_t id = ~cur;
       const DevTri T = S.tris[id];
-      const TriHit h = cramer(d, T.nab.xyz, T.nac.xyz, T.v0.xyz - o, T.nrm.xyz, tmin);
+      const TriHit h = cramer(d, T.nab.xyz, T.nac.xyz, T.v0.xyz - o, tri_normal(T.v0, T.nab, T.nac), tmin);
       tr.tests++;
       if (h.accept) {
         tr.last = id;
@@ -504,8 +523,10 @@ __device__ inline Trace traverse_exact(const SceneView &S, f3 o, f3 d, float tmi
       if (cur != kDone) {
         const int32_t id = ~cur;
         const DevTri T = S.tris[id];
-        const TriHit h = cramer_reduced(d, T.nab.xyz, T.nac.xyz, T.v0.xyz - o, T.nrm.xyz, T.v0.w, T.nab.w,
-                                        T.nac.w, tmin);
+        float m_x1, m_y4, m_y8;
+        tri_minors(T.nab.xyz, T.nac.xyz, m_x1, m_y4, m_y8);
+        const TriHit h = cramer_reduced(d, T.nab.xyz, T.nac.xyz, T.v0.xyz - o, tri_normal(T.v0, T.nab, T.nac), m_x1,
+                                        m_y4, m_y8, tmin);
         tr.tests++;
         if (h.accept) {
           tr.last = id;
@@ -1209,10 +1230,15 @@ __global__ void __launch_bounds__(64, MCPT_WAVES_PER_SIMD) k_render(RenderArgs A
           tri_arr = S.triq;
         else
           tri_arr = S.tris;
-        const Tri T = tri_arr[MCPT_DCHECK(~cur < S.n_tris, 2) ? ~cur : 0];
+        const int32_t ti = MCPT_DCHECK(~cur < S.n_tris, 2) ? ~cur : 0;
+        const Tri T = tri_arr[ti];
         Tri T2;
-        if (two) T2 = tri_arr[MCPT_DCHECK(~nx < S.n_tris, 2) ? ~nx : 0];
-        auto test = [&](const Tri &X) {
+        int32_t ti2 = 0;
+        if (two) {
+          ti2 = MCPT_DCHECK(~nx < S.n_tris, 2) ? ~nx : 0;
+          T2 = tri_arr[ti2];
+        }
+        auto test = [&](const Tri &X, int32_t xi) {
           TriHit h;
           if constexpr (Q) {
             // the reference leaf's own box (hlbvh.cpp:97-100: min/max of the
@@ -1229,13 +1255,23 @@ __global__ void __launch_bounds__(64, MCPT_WAVES_PER_SIMD) k_render(RenderArgs A
             h.accept = h.accept && leaf;
             if (STATS) n_rej += !leaf;
           } else {
-            h = LIT ? cramer(d.xyz, X.nab.xyz, X.nac.xyz, X.v0.xyz - o.xyz, X.nrm.xyz, kTmin)
-                    : cramer_reduced(d.xyz, X.nab.xyz, X.nac.xyz, X.v0.xyz - o.xyz, X.nrm.xyz, X.v0.w, X.nab.w,
-                                     X.nac.w, kTmin);
+            const f3 xn = tri_normal(X.v0, X.nab, X.nac);
+            if (LIT) {
+              h = cramer(d.xyz, X.nab.xyz, X.nac.xyz, X.v0.xyz - o.xyz, xn, kTmin);
+            } else {
+              float m_x1, m_y4, m_y8;
+              tri_minors(X.nab.xyz, X.nac.xyz, m_x1, m_y4, m_y8);
+              h = cramer_reduced(d.xyz, X.nab.xyz, X.nac.xyz, X.v0.xyz - o.xyz, xn, m_x1, m_y4, m_y8, kTmin);
+            }
           }
           if (STATS) n_tests++;
           if (h.accept) {
-            if (ref ? best_t - h.t >= kEps : h.t < best_t) best_nrm = X.nrm;  // objdef.h:213
+            if (ref ? best_t - h.t >= kEps : h.t < best_t) {  // objdef.h:213
+              if constexpr (Q)
+                best_nrm = X.nrm;
+              else
+                best_nrm = (f4){X.v0.w, X.nab.w, X.nac.w, as_f(~xi)};  // the material is read at shading
+            }
             if (ref) {
               if (best_t - h.t >= kEps) best_t = h.t;
             } else {
@@ -1243,10 +1279,10 @@ __global__ void __launch_bounds__(64, MCPT_WAVES_PER_SIMD) k_render(RenderArgs A
             }
           }
         };
-        test(T);
+        test(T, ti);
         if (two) {
           (void)stk.pop(sp);
-          test(T2);
+          test(T2, ti2);
         }
         cur = pop_next();
       }
@@ -1265,7 +1301,11 @@ __global__ void __launch_bounds__(64, MCPT_WAVES_PER_SIMD) k_render(RenderArgs A
         cur = S.root_leaf >= 0 ? ~S.root_leaf : 0;  // the root box passed: there were hits
       } else if (PRIM && in_s) {
         PrimHit h;
-        h.nrm = best_t < kFltMax ? best_nrm : (f4){0.0f, 0.0f, 0.0f, 0.0f};
+        h.nrm = (f4){0.0f, 0.0f, 0.0f, 0.0f};
+        if (best_t < kFltMax) {
+          h.nrm = best_nrm;
+          if (!Q) h.nrm.w = as_f(hit_material(S.tris, as_i(best_nrm.w)));  // the record carries the material
+        }
         h.t = best_t;
         const f4 v = U->cam.camera_type == 0 ? d : o;
         h.ray[0] = v.x, h.ray[1] = v.y, h.ray[2] = v.z;
@@ -1287,7 +1327,7 @@ __global__ void __launch_bounds__(64, MCPT_WAVES_PER_SIMD) k_render(RenderArgs A
           in.nrm = (f4){tn.x, tn.y, tn.z, 0.0f};
           if (cl_dot3(d.xyz, in.nrm.xyz) > 0) in.nrm = -in.nrm;  // intersect.cl:23-25
           in.pt = o + best_t * d;                                  // objdef.h:218
-          in.mat = as_i(tn.w);
+          in.mat = Q ? as_i(tn.w) : hit_material(S.tris, as_i(tn.w));
           bool rs = G && lst == kRes;
           ShadeOut so;
           if (A.lds_mats)  // LDS-typed reads (ds_read, no flat access waiting on vector memory)
@@ -1428,9 +1468,9 @@ __global__ void __launch_bounds__(64) k_intersect(SceneView S, const mcpt_ray *r
   h.pad = 0;
   if (tr.tri >= 0) {
     const DevTri &T = S.tris[tr.tri];
-    nrm = (f4){T.nrm.x, T.nrm.y, T.nrm.z, 0.0f};
+    nrm = (f4){T.v0.w, T.nab.w, T.nac.w, 0.0f};
     pt = o + tr.t * d;
-    h.material_id = (uint32_t)as_i(T.nrm.w);
+    h.material_id = (uint32_t)as_i(T.aux.x);
   }
   if (tr.last >= 0) {
     h.triangle_id = (uint32_t)(MODE == MCPT_MODE_NOPRUNE ? tr.last : tr.tri);
@@ -1464,7 +1504,11 @@ __global__ void __launch_bounds__(64) k_primary(RenderArgs A, PrimHit *out) {
                                              : traverse_exact(A.S, o.xyz, d.xyz, kTmin, lds_stack + threadIdx.x, 64,
                                                               fallbacks);
   PrimHit h;
-  h.nrm = tr.tri >= 0 ? A.S.tris[tr.tri].nrm : (f4){0.0f, 0.0f, 0.0f, 0.0f};
+  h.nrm = (f4){0.0f, 0.0f, 0.0f, 0.0f};
+  if (tr.tri >= 0) {
+    const DevTri &T = A.S.tris[tr.tri];
+    h.nrm = (f4){T.v0.w, T.nab.w, T.nac.w, T.aux.x};
+  }
   h.t = tr.t;
   const f4 v = A.cam.camera_type == 0 ? d : o;
   h.ray[0] = v.x, h.ray[1] = v.y, h.ray[2] = v.z;
@@ -2057,10 +2101,10 @@ int mcpt_scene_upload(mcpt_ctx *ctx, const mcpt_triangle *tris, int64_t n_tris, 
     const float b1 = -(t.v[1][0] - t.v[0][0]), b2 = -(t.v[1][1] - t.v[0][1]), b3 = -(t.v[1][2] - t.v[0][2]);
     const float c1 = -(t.v[2][0] - t.v[0][0]), c2 = -(t.v[2][1] - t.v[0][1]), c3 = -(t.v[2][2] - t.v[0][2]);
     // triangle-only minors of cramer_reduced (std::fma = the device's fused v_fma_f32)
-    d.v0 = (f4){t.v[0][0], t.v[0][1], t.v[0][2], std::fma(b2, c3, -(c2 * b3))};
-    d.nab = (f4){b1, b2, b3, std::fma(b1, c3, -(c1 * b3))};
-    d.nac = (f4){c1, c2, c3, std::fma(b1, c2, -(c1 * b2))};
-    d.nrm = (f4){t.normal[0], t.normal[1], t.normal[2], t.normal[3]};
+    d.v0 = (f4){t.v[0][0], t.v[0][1], t.v[0][2], t.normal[0]};
+    d.nab = (f4){b1, b2, b3, t.normal[1]};
+    d.nac = (f4){c1, c2, c3, t.normal[2]};
+    d.aux = (f4){t.normal[3], std::fma(b2, c3, -(c2 * b3)), std::fma(b1, c3, -(c1 * b3)), std::fma(b1, c2, -(c1 * b2))};
   }
   // The quantized search tree: 64-B nodes whose decoded
   // boxes strictly contain the exact ones, so every box test is a superset of
@@ -2090,10 +2134,10 @@ int mcpt_scene_upload(mcpt_ctx *ctx, const mcpt_triangle *tris, int64_t n_tris, 
     tq.resize(n);
     for (int64_t i = 0; i < n; ++i) {
       const mcpt_triangle &t = tris[i];
-      tq[i].v0 = (f4){t.v[0][0], t.v[0][1], t.v[0][2], dt[i].v0.w};
-      tq[i].v1 = (f4){t.v[1][0], t.v[1][1], t.v[1][2], dt[i].nab.w};
-      tq[i].v2 = (f4){t.v[2][0], t.v[2][1], t.v[2][2], dt[i].nac.w};
-      tq[i].nrm = dt[i].nrm;
+      tq[i].v0 = (f4){t.v[0][0], t.v[0][1], t.v[0][2], dt[i].aux.y};
+      tq[i].v1 = (f4){t.v[1][0], t.v[1][1], t.v[1][2], dt[i].aux.z};
+      tq[i].v2 = (f4){t.v[2][0], t.v[2][1], t.v[2][2], dt[i].aux.w};
+      tq[i].nrm = (f4){t.normal[0], t.normal[1], t.normal[2], t.normal[3]};
     }
   } else {
     nq.clear();

@@ -144,11 +144,11 @@ __global__ void k_tris(const mcpt_triangle *__restrict__ tris, int64_t n, UDevTr
   const float b1 = -(t.v[1][0] - t.v[0][0]), b2 = -(t.v[1][1] - t.v[0][1]), b3 = -(t.v[1][2] - t.v[0][2]);
   const float c1 = -(t.v[2][0] - t.v[0][0]), c2 = -(t.v[2][1] - t.v[0][1]), c3 = -(t.v[2][2] - t.v[0][2]);
   const float m0 = fmaf(b2, c3, -(c2 * b3)), m1 = fmaf(b1, c3, -(c1 * b3)), m2 = fmaf(b1, c2, -(c1 * b2));
-  UDevTri d;
-  d.v0[0] = t.v[0][0], d.v0[1] = t.v[0][1], d.v0[2] = t.v[0][2], d.v0[3] = m0;
-  d.v1[0] = b1, d.v1[1] = b2, d.v1[2] = b3, d.v1[3] = m1;
-  d.v2[0] = c1, d.v2[1] = c2, d.v2[2] = c3, d.v2[3] = m2;
-  for (int k = 0; k < 4; ++k) d.nrm[k] = t.normal[k];
+  UDevTri d;  // DevTri: the normal's xyz in the .w lanes, aux = (material bits, minors)
+  d.v0[0] = t.v[0][0], d.v0[1] = t.v[0][1], d.v0[2] = t.v[0][2], d.v0[3] = t.normal[0];
+  d.v1[0] = b1, d.v1[1] = b2, d.v1[2] = b3, d.v1[3] = t.normal[1];
+  d.v2[0] = c1, d.v2[1] = c2, d.v2[2] = c3, d.v2[3] = t.normal[2];
+  d.nrm[0] = t.normal[3], d.nrm[1] = m0, d.nrm[2] = m1, d.nrm[3] = m2;
   dt[i] = d;
   UDevTri q;
   for (int k = 0; k < 3; ++k) q.v0[k] = t.v[0][k], q.v1[k] = t.v[1][k], q.v2[k] = t.v[2][k];
