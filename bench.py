@@ -212,12 +212,38 @@ def load_profile(workload, steps):
         return None
 
 
-def timed_render(rnd, dsc, cam, st, steps, warmup, kw, ws, shared):
+ATTEMPT = 1 << 30  # accumulate every frame (the reference's MAX_ATTEMPT cap never binds here)
+
+
+def tune_plan(rnd, dsc, cam, st, steps, kw, schedule="auto", shade_threshold=0, depth=None):
+    """The launch-plan pick main() makes before the warmup (untimed; every
+    setting gives the same bits): with schedule "auto", Renderer.tune over the
+    leaf schedule, S and fetch thresholds, block sizing, tile order and last
+    block on calls of the timed call's size, 5 trials each, every trial a
+    fresh view (primary-hit pass and tile sort included, as in the timed
+    call).  tests/test_gpu_fullsize.py runs this same function before
+    comparing the timed call with the reference kernels.  Returns the S
+    threshold in force."""
+    from montecarlopathtracing_amd import _lib as L
+    depth = DEPTH if depth is None else depth
+    frames = max(1, min(steps, 64))
+    shade_th = rnd.get_tuning()["shade_threshold"] or 32
+    if schedule == "auto" and shade_threshold > 0:
+        rnd.tune_schedule(dsc, cam, st, depth, ATTEMPT, frames=frames, trials=5, **kw)
+    elif schedule == "auto":
+        _, shade_th, _ = rnd.tune(dsc, cam, st, depth, ATTEMPT, frames=frames, trials=5, fresh_view=True, **kw)
+    else:
+        dsc.schedule = L.SCHED_PAIRED if schedule == "paired" else L.SCHED_SINGLE
+    return shade_th
+
+
+def timed_render(rnd, dsc, cam, st, steps, warmup, kw, ws, shared, depth=None, per_rank=False):
     """W untimed warmup frames, then K frames timed between barrier +
-    synchronize on both sides; returns (elapsed s, max over ranks)."""
-    attempt = 1 << 30  # accumulate every frame (the reference's MAX_ATTEMPT cap never binds here)
+    synchronize on both sides; returns the elapsed seconds, the max over
+    ranks (per_rank: also every rank's own elapsed seconds)."""
+    depth = DEPTH if depth is None else depth
     if warmup > 0:
-        rnd.render_frames(dsc, cam, st, DEPTH, attempt, warmup, **kw)
+        rnd.render_frames(dsc, cam, st, depth, ATTEMPT, warmup, **kw)
     torch.cuda.synchronize()
     # the timed call computes its own primary hits (k_primary runs inside the
     # timed region): nothing the warmup computed is reused
@@ -226,16 +252,56 @@ def timed_render(rnd, dsc, cam, st, steps, warmup, kw, ws, shared):
         torch.distributed.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    rnd.render_frames(dsc, cam, st, DEPTH, attempt, steps, **kw)
+    rnd.render_frames(dsc, cam, st, depth, ATTEMPT, steps, **kw)
     torch.cuda.synchronize()
+    own = time.perf_counter() - t0  # this rank's own share, before waiting for the others
     if ws > 1:
         torch.distributed.barrier()
     elapsed = time.perf_counter() - t0
+    ranks = [own]
     if ws > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device="cpu" if shared else rnd.device)
+        dev = "cpu" if shared else rnd.device
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
         elapsed = float(t.item())
-    return elapsed
+        if per_rank:
+            mine = torch.tensor([own], dtype=torch.float64, device=dev)
+            allt = [torch.zeros_like(mine) for _ in range(ws)]
+            torch.distributed.all_gather(allt, mine)
+            ranks = [float(x.item()) for x in allt]
+    return (elapsed, ranks) if per_rank else elapsed
+
+
+def one_gpu_time(rnd, dsc, cam, w, h, steps, warmup, ws, rank, depth=None, frames_per_launch=0):
+    """The strong-scaled image rendered whole on ONE GPU inside the same job
+    (rank 0; the other ranks wait at a barrier), timed like timed_render:
+    the denominator of strong_scaling.speedup_vs_1gpu.  Same tuning as the
+    shares' call; returns seconds on rank 0, None elsewhere."""
+    if ws > 1:
+        torch.distributed.barrier()
+    out = None
+    if rank == 0:
+        st1 = rnd.new_state(w, h, default_seeds(w * h))
+        out = timed_render(rnd, dsc, cam, st1, steps, warmup,
+                           dict(stripe_rows=STRIPE_ROWS, stripe_index=0, stripe_count=1,
+                                frames_per_launch=frames_per_launch), 1, True, depth=depth)
+        del st1
+    if ws > 1:
+        torch.distributed.barrier()
+    return out
+
+
+def strong_record(w, h, steps, elapsed, ranks, one_s, note):
+    """strong_scaling: the fixed image's rate over the ranks, each rank's own
+    share time, and the speed-up over the same image on one GPU in this job."""
+    return {"value": round(float(w * h) * steps * DEPTH / elapsed / 1e6, 2), "unit": "Msamples/s",
+            "ms_per_step": round(elapsed * 1e3 / steps, 4), "image": [w, h],
+            "share_ms_per_rank": [round(x * 1e3, 3) for x in ranks],
+            "share_max_over_mean": round(max(ranks) / (sum(ranks) / len(ranks)), 4),
+            "one_gpu_ms": None if one_s is None else round(one_s * 1e3, 3),
+            "one_gpu_value": None if one_s is None else round(float(w * h) * steps * DEPTH / one_s / 1e6, 2),
+            "speedup_vs_1gpu": None if one_s is None else round(one_s / elapsed, 4),
+            "note": note}
 
 
 def main():
@@ -301,7 +367,7 @@ def main():
     seeds = default_seeds(W * h_img)
     st = rnd.new_state(W, h_img, seeds)
     kw = dict(stripe_rows=STRIPE_ROWS, stripe_index=rank, stripe_count=n, frames_per_launch=args.frames_per_launch)
-    attempt = 1 << 30
+    attempt = ATTEMPT
     # leaf-test schedule (identical images; speed only), chosen before any timing
     if args.shade_threshold > 0:
         rnd.set_tuning(**dict(rnd.get_tuning(), shade_threshold=args.shade_threshold))
@@ -315,19 +381,10 @@ def main():
         rnd.set_tuning(**dict(rnd.get_tuning(), tile_order=args.tile_order))
     if args.quantized:
         rnd.set_tuning(**dict(rnd.get_tuning(), quantized=args.quantized))
-    shade_th = rnd.get_tuning()["shade_threshold"] or 32
-    if args.schedule == "auto" and args.shade_threshold > 0:
-        rnd.tune_schedule(dsc, cam, st, DEPTH, attempt, frames=max(1, min(args.steps, 64)), trials=5, **kw)
-    elif args.schedule == "auto":
-        # timed on calls of the timed call's size (same frame-block regime), 3 trials each
-        # and the S-phase threshold (speed only; every setting gives the same bits)
-        # each trial as the timed call runs: a fresh view (primary-hit pass and tile sort included)
-        _, shade_th, _ = rnd.tune(dsc, cam, st, DEPTH, attempt, frames=max(1, min(args.steps, 64)), trials=5,
-                                  fresh_view=True, **kw)
-    else:
-        dsc.schedule = L.SCHED_PAIRED if args.schedule == "paired" else L.SCHED_SINGLE
+    shade_th = tune_plan(rnd, dsc, cam, st, args.steps, kw, schedule=args.schedule,
+                         shade_threshold=args.shade_threshold)
 
-    elapsed = timed_render(rnd, dsc, cam, st, args.steps, args.warmup, kw, ws, shared)
+    elapsed, rank_s = timed_render(rnd, dsc, cam, st, args.steps, args.warmup, kw, ws, shared, per_rank=True)
     kst = rnd.stats()
     # the same frames with the primary-hit cache off (every frame traces its
     # primary ray), timed after the headline: the memoization's share of it
@@ -406,13 +463,30 @@ def main():
         torch.distributed.barrier()
         reduce_ms = (time.perf_counter() - t1) * 1e3
         if not args.no_strong and not strong_only:
-            # strong scaling: the fixed 1024x1024 image striped over the ranks
+            # strong scaling: the fixed 1024x1024 image striped over the ranks,
+            # then the same image on one GPU (rank 0) in this same job, with the
+            # headline's tuning (tuned on 1024x1024 pixels per GPU: the same
+            # pixel count as the whole image on one GPU)
             sts = rnd.new_state(W, H_PER_GPU, default_seeds(W * H_PER_GPU))
-            es = timed_render(rnd, dsc, cam, sts, args.steps, args.warmup, kw, ws, shared)
-            strong = {"value": round(float(W * H_PER_GPU) * args.steps * DEPTH / es / 1e6, 2), "unit": "Msamples/s",
-                      "ms_per_step": round(es * 1e3 / args.steps, 4), "image": [W, H_PER_GPU],
-                      "note": "the fixed 1024x1024 image striped over the ranks"}
+            es, es_ranks = timed_render(rnd, dsc, cam, sts, args.steps, args.warmup, kw, ws, shared, per_rank=True)
             del sts
+            one = one_gpu_time(rnd, dsc, cam, W, H_PER_GPU, args.steps, args.warmup, ws, rank,
+                               frames_per_launch=args.frames_per_launch)
+            strong = strong_record(W, H_PER_GPU, args.steps, es, es_ranks, one,
+                                   "the fixed 1024x1024 image striped over the ranks; speedup_vs_1gpu = the same "
+                                   "image and call rendered whole by rank 0 alone in this job / the striped time")
+        elif not args.no_strong and strong_only:
+            # C4: the headline IS the strong-scaled image; the one-GPU time of
+            # the same call in this job, with the library's auto plan (the
+            # tuning was picked for a share, not the whole image)
+            tuned = rnd.get_tuning()
+            rnd.set_tuning()
+            one = one_gpu_time(rnd, dsc, cam, W, h_img, args.steps, args.warmup, ws, rank,
+                               frames_per_launch=args.frames_per_launch)
+            rnd.set_tuning(**tuned)
+            strong = strong_record(W, h_img, args.steps, elapsed, rank_s, one,
+                                   "the headline's fixed image; speedup_vs_1gpu = the same image and call rendered "
+                                   "whole by rank 0 alone in this job (auto plan) / the striped time")
 
     total_samples = float(W * h_img) * args.steps * DEPTH
     value = total_samples / elapsed / 1e6

@@ -237,6 +237,13 @@ typedef struct mcpt_tuning {
 } mcpt_tuning;
 
 /* ------------------------------------------------------- version / errors */
+/* The ABI revision this header describes.  It changes whenever a struct
+ * passed across the boundary changes size or an entry point its arguments
+ * (3: mcpt_tuning's tile_order / pixel_spread, mcpt_set_pixel_segments'
+ * capacity).  A binding checks mcpt_abi_version() == MCPT_ABI_VERSION once
+ * at load and refuses a library built from another header.               */
+#define MCPT_ABI_VERSION 3
+int32_t mcpt_abi_version(void);
 const char *mcpt_version(void);
 const char *mcpt_last_error(void);
 
@@ -387,11 +394,14 @@ int mcpt_get_stats(mcpt_ctx *ctx, mcpt_stats *out);
  * (the chain of work its frames are, one sequential seed chain per pixel)
  * into counts_dev[y * width + x] and the k_render loop iterations its lane
  * spent on it into iters_dev (width*height u32 each on the device, zeroed by
- * the caller; either may be NULL); NULL, NULL stops it.                    */
-int mcpt_set_pixel_segments(mcpt_ctx *ctx, uint32_t *counts_dev, uint32_t *iters_dev);
+ * the caller; either may be NULL); NULL, NULL stops it.  n_pixels is the
+ * buffers' capacity in pixels: a call whose image has more pixels collects
+ * nothing (never writes past them).                                        */
+int mcpt_set_pixel_segments(mcpt_ctx *ctx, uint32_t *counts_dev, uint32_t *iters_dev, int64_t n_pixels);
 /* The primary-hit pass's per-pixel traversal cost of the cached view (loop
  * iterations of k_render's PRIM form, or node steps + triangle tests of
- * k_primary), width*height u32 to the host; *n = 0 when no cache is held. */
+ * k_primary), width*height u32 to the host; *n = 0 when no cache is held.
+ * Pixels outside the cached call's own row stripes read 0.                */
 int mcpt_get_primary_cost(mcpt_ctx *ctx, uint32_t *out, int64_t cap, int64_t *n);
 
 /* Diagnostics (MCPT_PHASE_TIMING builds, libmcpt_hip_timing.so): the

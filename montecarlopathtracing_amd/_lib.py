@@ -28,6 +28,7 @@ BVHNODE = np.dtype([("bbmin", "<f4", 4), ("bbmax", "<f4", 4), ("pad", "<f4", 4),
 for _dt, _sz in ((CAMERA, 80), (RAY, 48), (HIT, 48), (TRIANGLE, 64), (MATERIAL, 48), (BVHNODE, 64)):
     assert _dt.itemsize == _sz
 
+ABI_VERSION = 3  # include/mcpt_hip.h MCPT_ABI_VERSION
 MCPT_DIFFUSE, MCPT_GLOSSY, MCPT_TRANSPARENT, MCPT_LIGHT = 1, 2, 3, 4
 MODE_EXACT, MODE_NOPRUNE = 0, 1
 SCHED_SINGLE, SCHED_PAIRED = 0, 1  # mcpt_render_params.schedule
@@ -73,6 +74,7 @@ _S = ctypes.c_char_p
 
 # name -> (restype, argtypes); every symbol include/mcpt_hip.h declares
 SIGNATURES = {
+    "mcpt_abi_version": (_I32, []),
     "mcpt_version": (_S, []),
     "mcpt_last_error": (_S, []),
     "mcpt_parse_camera": (_I32, [_P, _P, _P, _D, _P]),
@@ -107,7 +109,7 @@ SIGNATURES = {
     "mcpt_set_stats": (_I32, [_P, _I32]),
     "mcpt_get_stats": (_I32, [_P, _P]),
     "mcpt_get_wave_log": (_I32, [_P, _P, _I64, _P]),
-    "mcpt_set_pixel_segments": (_I32, [_P, _P, _P]),
+    "mcpt_set_pixel_segments": (_I32, [_P, _P, _P, _I64]),
     "mcpt_get_primary_cost": (_I32, [_P, _P, _I64, _P]),
     "mcpt_get_entry_log": (_I32, [_P, _P, _I64, _P, _P]),
     "mcpt_selfcheck_trig": (_I32, [_P, _P, _P]),
@@ -147,6 +149,9 @@ def lib():
             fn = getattr(so, name)
             fn.restype = res
             fn.argtypes = args
+        if hasattr(so, "mcpt_abi_version") and so.mcpt_abi_version() != ABI_VERSION:
+            raise MCPTError("libmcpt_hip.so implements ABI %d, this binding ABI %d (rebuild one of them)" % (
+                so.mcpt_abi_version(), ABI_VERSION))
         _lib = so
     return _lib
 

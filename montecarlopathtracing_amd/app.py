@@ -84,10 +84,11 @@ class App:
         todo = frames
         if frames >= 4096 and not getattr(self, "_tuned", False):  # long runs: time the leaf schedules, S-phase
             # and fetch thresholds on one-block 16-frame calls (7 trials, 112 scratch frames, bit-identical
-            # either way).  Not the block sizing: a long call runs max_block_frames-frame blocks whatever
-            # block_entries says, so short trials of it would tune a regime the run never enters.
+            # either way).  Not the block sizing nor the tile order: a long call runs max_block_frames-frame
+            # blocks whatever block_entries says, and the tile order mostly shortens a launch's tail, so
+            # one-block trials of either would tune a regime the run never enters.
             self.renderer.tune(self.scene, self.camera, self.state, self.cfg.MAXDEPTH(), att, frames=16,
-                               block_entries=None, last_block=False, frames_per_launch=16)
+                               block_entries=None, last_block=False, tile_orders=None, frames_per_launch=16)
             self._tuned = True
         while todo > 0:
             n = todo if self.attempt_count > att else min(todo, att + 1 - self.attempt_count)

@@ -240,6 +240,7 @@ struct mcpt_ctx {
   bool stats_on = false;
   uint32_t *px_segments = nullptr;        // mcpt_set_pixel_segments (stats calls only)
   uint32_t *px_iters = nullptr;
+  int64_t px_cap = 0;                     // their capacity in pixels (a larger image collects nothing)
   unsigned long long *d_stats = nullptr;  // segments, nodes, tris, bad, wave T/L/S phases
   uint32_t *d_queue = nullptr;            // k_render work-queue heads, kQueues per launch
   int32_t queue_cap = 0;                  // launches the head array holds
@@ -1614,9 +1615,11 @@ __global__ void k_gamma_preview(const f4 *color, f4 *out, int64_t n) {  // out m
 // =================================================================== ABI
 extern "C" {
 
+int32_t mcpt_abi_version(void) { return MCPT_ABI_VERSION; }
+
 const char *mcpt_version(void) {
-  return kDebug ? "mcpt-mi355x 0.2 (gfx950, MCPT_DEBUG)"
-                : (kTiming ? "mcpt-mi355x 0.2 (gfx950, MCPT_PHASE_TIMING)" : "mcpt-mi355x 0.2 (gfx950)");
+  return kDebug ? "mcpt-mi355x 0.3 (gfx950, MCPT_DEBUG)"
+                : (kTiming ? "mcpt-mi355x 0.3 (gfx950, MCPT_PHASE_TIMING)" : "mcpt-mi355x 0.3 (gfx950)");
 }
 
 int mcpt_device_count(int32_t *count) {
@@ -1800,10 +1803,12 @@ int mcpt_set_stats(mcpt_ctx *c, int32_t on) {
   return MCPT_OK;
 }
 
-int mcpt_set_pixel_segments(mcpt_ctx *c, uint32_t *counts_dev, uint32_t *iters_dev) {
+int mcpt_set_pixel_segments(mcpt_ctx *c, uint32_t *counts_dev, uint32_t *iters_dev, int64_t n_pixels) {
   if (!c) return mcpt::fail(MCPT_ERR_ARG, "set_pixel_segments: null ctx");
+  if ((counts_dev || iters_dev) && n_pixels <= 0) return mcpt::fail(MCPT_ERR_ARG, "set_pixel_segments: no capacity");
   c->px_segments = counts_dev;
   c->px_iters = iters_dev;
+  c->px_cap = (counts_dev || iters_dev) ? n_pixels : 0;
   return MCPT_OK;
 }
 
@@ -2562,8 +2567,9 @@ int mcpt_render_frames(mcpt_ctx *ctx, const mcpt_scene *scene, const mcpt_camera
   A.handoff = ctx->d_handoff;
   A.spill = ctx->d_spill;
   A.wave_log = nullptr;
-  A.px_segments = ctx->stats_on ? ctx->px_segments : nullptr;
-  A.px_iters = ctx->stats_on ? ctx->px_iters : nullptr;
+  const bool px_fit = ctx->stats_on && n_px <= ctx->px_cap;  // never past the caller's buffers
+  A.px_segments = px_fit ? ctx->px_segments : nullptr;
+  A.px_iters = px_fit ? ctx->px_iters : nullptr;
   A.prim_cost = nullptr;  // set where the primary-hit pass runs
   ctx->wave_log_n = 0;
   if (kTiming) {  // diagnostics: each launch's workgroups log their timeline (the last launch's remain)
@@ -2644,6 +2650,9 @@ int mcpt_render_frames(mcpt_ctx *ctx, const mcpt_scene *scene, const mcpt_camera
           ctx->prim_cap = n_px;
         }
         A.prim_cost = ctx->d_prim_cost;
+        // the pass writes its own stripes' costs only: zero the others, so
+        // the tile keys and mcpt_get_primary_cost never read stale words
+        if (p->stripe_count > 1) HIP_OK(hipMemsetAsync(ctx->d_prim_cost, 0, (size_t)n_px * sizeof(uint32_t), st));
         if (scene->near4_bytes <= kPrimSmallTree) {
           // small trees: one ray per lane, one 8x8 tile per workgroup
           const size_t lds_p = (size_t)depth_entries * 64 * sizeof(int32_t);

@@ -69,9 +69,10 @@ def render_distributed(renderer, scene, camera, width, height, max_depth, max_at
     st = renderer.new_state(width, height, seeds)
     kw = dict(stripe_rows=stripe_rows, stripe_index=rank, stripe_count=world, mode=mode)
     if frames >= 4096:  # long runs: each rank times the leaf schedules and S/fetch thresholds on one-block
-        # 16-frame calls (same bits; block sizing is not tuned: long calls run max_block_frames blocks, App.update)
+        # 16-frame calls (same bits; neither block sizing nor tile order is tuned: long calls run
+        # max_block_frames blocks, a regime one-block trials do not enter, App.update)
         renderer.tune(scene, camera, st, max_depth, max_attempt, frames=16, block_entries=None, last_block=False,
-                      frames_per_launch=16, **kw)
+                      tile_orders=None, frames_per_launch=16, **kw)
     renderer.render_frames(scene, camera, st, max_depth, max_attempt, frames, **kw)
     torch.cuda.synchronize()
     mask = ownership_mask(width, height, stripe_rows, rank, world)

@@ -149,8 +149,9 @@ class Renderer:
         CUDA tensors of width*height, zeroed by the caller; None: not
         collected)."""
         self._px_counts = (counts, iters)  # kept alive while the library holds the pointers
+        n = min([t.numel() for t in (counts, iters) if t is not None], default=0)
         L.check(L.lib().mcpt_set_pixel_segments(self.ctx, None if counts is None else L.ptr(counts),
-                                                None if iters is None else L.ptr(iters)))
+                                                None if iters is None else L.ptr(iters), n))
 
     def primary_cost(self):
         """mcpt_get_primary_cost: the cached view's per-pixel primary-ray

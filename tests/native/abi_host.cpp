@@ -170,6 +170,8 @@ struct App {
     const Json &jc = c["camera"];
     if (jc.has("resolution") && ((int32_t)jc["resolution"][0].num != width || (int32_t)jc["resolution"][1].num != height))
       throw std::runtime_error("camera.resolution must equal width/height");
+    if (mcpt_abi_version() != MCPT_ABI_VERSION)  // a library built from another header: refuse it
+      throw std::runtime_error("libmcpt_hip.so ABI mismatch");
     OK(mcpt_ctx_create(0, &ctx));
     // ThirdPartyWrapper::loadObject, two-call sizing
     std::string dir = root + "/" + c["directory"].str;

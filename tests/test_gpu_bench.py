@@ -44,7 +44,12 @@ def test_bench_two_ranks_rehearsal():
     assert j["n_gpus"] == 2 and j["steps"] == 4 and j["scaling"] == "weak"
     assert j["value"] > 0 and j["config"]["parallelism"] == "row-stripe tiles x2"
     assert j["config"]["width"] == 1024 and j["config"]["height"] == 2048
-    assert j["strong_scaling"]["value"] > 0 and j["strong_scaling"]["image"] == [1024, 1024]
+    s = j["strong_scaling"]
+    assert s["value"] > 0 and s["image"] == [1024, 1024]
+    # the one-GPU time of the same image inside the job, and every rank's share
+    assert s["one_gpu_ms"] > 0 and s["speedup_vs_1gpu"] > 0 and s["one_gpu_value"] > 0
+    assert len(s["share_ms_per_rank"]) == 2 and all(x > 0 for x in s["share_ms_per_rank"])
+    assert s["share_max_over_mean"] >= 1.0
     assert j["cpu_baseline"] is None  # rank 0 at N=1 only
     assert j["image_reduce_ms"] is not None and j["image_reduce_ms"] > 0  # the final image reduce ran
     # the host dump (device-to-host copy of rank 0's image state), timed outside value
@@ -59,7 +64,10 @@ def test_bench_c4_strong_two_ranks_rehearsal():
                        capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stderr[-3000:]
     j = _lines(r.stdout)[0]
-    assert j["scaling"] == "strong" and j["config"]["height"] == 1080 and j["strong_scaling"] is None
+    assert j["scaling"] == "strong" and j["config"]["height"] == 1080
+    s = j["strong_scaling"]  # the headline's own image: its one-GPU time and shares
+    assert s["image"] == [1920, 1080] and s["value"] == j["value"]
+    assert s["one_gpu_ms"] > 0 and s["speedup_vs_1gpu"] > 0 and len(s["share_ms_per_rank"]) == 2
     assert j["image_reduce_ms"] is not None
 
 

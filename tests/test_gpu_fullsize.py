@@ -1,0 +1,161 @@
+"""GPU parity at the sizes the metric is quoted on: the HIP path against the
+reference's own OpenCL kernels (oracle/_ref, tests/refgpu.py: the unmodified
+rayGenerator/intersect/shade/history.cl replayed as OpenCL::update,
+MCPT/OpenCLApp.cpp:57-82) at every config's own image size, over the tree
+every reference render traverses (the GPU treelet pass, scenebuild.cpp:87-95).
+
+- C2: bench.py's exact headline call -- bench.tune_plan (Renderer.tune with
+  fresh_view, 5 trials per setting), then bench.timed_render (warmup 5, the
+  timed 20-frame call with its own primary-hit pass and tile sort) at
+  1024x1024, depth 8, MAX_ATTEMPT 2^30 -- against 25 reference frames.
+- C3 (veach_mis 1024x1024, depth 12) and C4 (dining proxy 1920x1080,
+  depth 16) through the same bench functions at a few frames.
+- C5: the full 10 M-triangle GPU-treelet tree: its left-first DFS stack depth
+  fits the reference's unchecked int stack[64] (objdef.h:247), and a 128x128
+  depth-8 render over the whole tree matches.
+
+Bar: bit-exact hist, count and seed chains.
+"""
+import time
+
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+
+pytestmark = pytest.mark.gpu
+
+import bench  # noqa: E402
+from montecarlopathtracing_amd import _lib as L  # noqa: E402
+from montecarlopathtracing_amd import render as R  # noqa: E402
+from montecarlopathtracing_amd import scene as S  # noqa: E402
+
+from . import refgpu  # noqa: E402
+
+needs_ref = pytest.mark.skipif(not refgpu.available(), reason="oracle/_ref not built (needs /root/reference at build time)")
+
+
+@pytest.fixture(scope="module")
+def rnd():
+    r = R.Renderer(0)
+    yield r
+    r.close()
+
+
+def _bits_equal(mine, ref, what):
+    a, b = np.ascontiguousarray(mine), np.ascontiguousarray(ref)
+    same = (a.view(np.uint8).reshape(len(a), -1) == b.view(np.uint8).reshape(len(b), -1)).all(axis=1)
+    if not same.all():
+        bad = np.flatnonzero(~same)
+        raise AssertionError("%s: %d / %d pixels differ, first %s" % (what, len(bad), len(a), bad[:8]))
+
+
+def _check(st, ref, what):
+    rh, rc, rs = ref
+    _bits_equal(st.count.cpu().numpy(), rc, what + " count")
+    _bits_equal(st.seeds_np(), rs, what + " seeds")
+    _bits_equal(st.hist.cpu().numpy(), rh, what + " hist")
+
+
+def _bench_call(rnd, workload, steps, warmup):
+    """bench.py main()'s path for one workload at N = 1: its scene (over the
+    GPU treelet tree), upload, plan tuning and timed call; returns (scene
+    data, camera, state after warmup + steps frames, the plan picked)."""
+    wl = bench.WORKLOADS[workload]
+    w, h, depth = wl["w"], wl["h"], wl["depth"]
+    data, camj = bench.load_scene(workload)
+    cam = S.parse_camera(camj)
+    dsc, _ = bench.upload_scene(rnd, data)
+    seeds = bench.default_seeds(w * h)
+    st = rnd.new_state(w, h, seeds)
+    kw = dict(stripe_rows=bench.STRIPE_ROWS, stripe_index=0, stripe_count=1, frames_per_launch=0)
+    base = rnd.get_tuning()
+    try:
+        bench.tune_plan(rnd, dsc, cam, st, steps, kw, depth=depth)
+        plan = dict(rnd.get_tuning(), schedule=dsc.schedule)
+        bench.timed_render(rnd, dsc, cam, st, steps, warmup, kw, 1, False, depth=depth)
+        plan["frames_per_block"] = rnd.stats()["frames_per_block"]
+        torch.cuda.synchronize()
+    finally:
+        rnd.set_tuning(**base)
+        dsc.close()
+    return data, cam, st, seeds, plan
+
+
+def _ref_render(data, cam, w, h, depth, frames, seeds):
+    t0 = time.perf_counter()
+    out = refgpu.render(data, cam, w, h, depth, frames, bench.ATTEMPT, seeds)
+    print("reference kernels: %dx%d depth %d, %d frames: %.1f s" % (w, h, depth, frames, time.perf_counter() - t0))
+    return out
+
+
+@needs_ref
+def test_c2_headline_call_bitexact(rnd):
+    """The driver's command (bench.py --steps 20 --warmup 5): the tuned plan
+    (whatever the tuner picks: every pick must give the reference's bits),
+    dearest-first tiles, 8 XCD queues with stealing and cross-XCD hand-offs,
+    the short last block, at 1024x1024 depth 8."""
+    data, cam, st, seeds, plan = _bench_call(rnd, "C2", 20, 5)
+    ref = _ref_render(data, cam, 1024, 1024, 8, 25, seeds)
+    _check(st, ref, "C2 bench call %r" % plan)
+    assert (ref[1] > 0).mean() > 0.5  # most pixels saw the light
+
+
+@needs_ref
+def test_c3_full_size_bitexact(rnd):
+    """C3: veach_mis at 1024x1024, depth 12 (glossy lobes, emitters), the
+    bench path's tuned plan, 1 warmup + 4 timed frames."""
+    data, cam, st, seeds, plan = _bench_call(rnd, "C3", 4, 1)
+    ref = _ref_render(data, cam, 1024, 1024, 12, 5, seeds)
+    _check(st, ref, "C3 %r" % plan)
+
+
+@needs_ref
+def test_c4_full_size_bitexact(rnd):
+    """C4: the dining proxy at 1920x1080, depth 16, the bench path's tuned
+    plan, 1 warmup + 2 timed frames."""
+    data, cam, st, seeds, plan = _bench_call(rnd, "C4", 2, 1)
+    ref = _ref_render(data, cam, 1920, 1080, 16, 3, seeds)
+    _check(st, ref, "C4 %r" % plan)
+
+
+@needs_ref
+def test_c5_full_tree_bitexact(rnd):
+    """C5: the full 10 M-triangle scene, its HLBVH and GPU treelet pass built
+    on the GPU as bench.upload_scene builds them.  The reference traverses
+    with an unchecked int stack[64] (objdef.h:247-270: a right child pushed
+    per internal node descended through); the tree's left-first stack depth
+    (mcpt_bvh_stack_depth, an upper bound on that stack's use) is within it,
+    so the reference is defined on C5.  A 128x128 depth-8 render over the
+    whole tree (auto: the 64-B quantized search tree; and the 128-B one)
+    matches the reference kernels bit for bit."""
+    data = S.random_mesh(10_000_000, build=lambda t: None)
+    dt = R.to_device(data.tris, 0)
+    dn = R.build_hlbvh_device(dt)
+    R.treelet_gpu_device(dn)
+    nodes = R.records(dn, L.BVHNODE).copy()
+    depth = S.bvh_stack_depth(nodes)
+    print("C5 GPU-treelet tree: %d nodes, left-first stack depth %d" % (len(nodes), depth))
+    assert depth <= 64, depth
+    cam = S.parse_camera(S.RANDOM_MESH_CAMERA)
+    w = h = 128
+    seeds = R.default_seeds(w * h)
+    base = rnd.get_tuning()
+    outs = []
+    try:
+        for quantized in (0, 2):
+            rnd.set_tuning(quantized=quantized)
+            dsc = rnd.upload((dt, dn, data.mats))
+            st = rnd.new_state(w, h, seeds)
+            rnd.render_frames(dsc, cam, st, 8, bench.ATTEMPT, 3, frames_per_launch=2)
+            outs.append((quantized, rnd.stats()["quantized"], st))
+            torch.cuda.synchronize()
+            dsc.close()
+    finally:
+        rnd.set_tuning(**base)
+    del dt, dn
+    assert [q for _, q, _ in outs] == [1, 0]  # auto took the quantized tree; 2 forced the 128-B one
+    ref = _ref_render(data.with_nodes(nodes), cam, w, h, 8, 3, seeds)
+    for quantized, _, st in outs:
+        _check(st, ref, "C5 full tree (quantized=%d)" % quantized)
+    assert (ref[1] > 0).any()

@@ -501,7 +501,12 @@ def test_short_last_block_same_bits(rnd, diffuse):
                 fpbs.append(rnd.stats()["frames_per_block"])
                 outs.append((st.hist.cpu().numpy(), st.count.cpu().numpy(), st.seeds_np()))
             assert fpbs[0] == 20 and fpbs[2] == 18, fpbs  # (18, 2): the short last block did run
-            assert fpbs[5] == 15, fpbs  # auto at 4 pixels per lane: (15, 5), a last block of ceil(20 / 4)
+            # the auto plan's regime follows the pixels per resident lane (the
+            # grid is the resident capacity): between 2.5 and 6 on a whole image
+            # it is (15, 5), a last block of ceil(20 / 4) (gfx950 today: 4 per lane)
+            ppl = float(w * h) / (rnd.stats()["workgroups"] * 64)
+            if 2.5 < ppl < 6.0:
+                assert fpbs[5] == 15, (fpbs, ppl)
             for o in outs[1:]:
                 for a, b, what in zip(outs[0], o, ("hist", "count", "seeds")):
                     assert_bits_equal(a, b, what)

@@ -15,7 +15,8 @@ Back here:
 
     python tools/profile.py summarize <tag>
 
-copies the CSVs to profiles/<tag>_*.csv and writes profiles/<tag>_summary.json
+copies the CSVs to profiles/<tag>_*.csv (trimmed to the timed dispatch's rows,
+tools/trim_profiles.py) and writes profiles/<tag>_summary.json
 plus the entry of profiles/pmc_summary.json that bench.py reads (keyed by
 workload and frames per call).  The timed launch is the LAST dispatch of the
 bench's non-counting k_render instantiation (bench order: schedule tuning,
@@ -276,6 +277,11 @@ def summarize(tag):
                                                     "td_busy_saturated_microbench", "busy_frac")}
     with open(path, "w") as fh:
         json.dump(allw, fh, indent=1, sort_keys=True)
+    # keep only the rows the summary is computed from (tools/trim_profiles.py):
+    # the timed dispatch of each --pmc pass, the render kernels of the trace
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    import trim_profiles
+    trim_profiles.main(sorted(glob.glob(os.path.join(dst, tag + "_*.csv"))))
     print(json.dumps(summ, indent=1))
 
 
