@@ -22,22 +22,24 @@ The timed call computes its own primary hits (k_primary, then k_render reads
 them at every frame start): nothing the warmup computed is reused.
 
 Also reported (rank 0; cpu_baseline at N=1 only):
-  roofline     — the hot kernel k_render against the unit that binds it: "td"
-                 (the vector-memory data path: the launch's gather floor from
-                 its own counters x the microbenchmark's per-instruction and
-                 per-line costs, as a share of its cycles) on the cache-resident
-                 scenes, "hbm" where HBM's fraction is the larger; both are
-                 reported (roofline.td, roofline.hbm).  traffic = memory-side
-                 bytes per launch (rocprofv3 FETCH_SIZE x the calibrated scale
-                 + WRITE_SIZE, the timed launch of this same command, committed
-                 in profiles/pmc_summary.json by tools/profile.py); achieved =
+  roofline     — the hot kernel k_render against HBM (bound "hbm", the
+                 contract's roofline): traffic = memory-side bytes per launch
+                 (rocprofv3 FETCH_SIZE x the calibrated scale + WRITE_SIZE of
+                 this same command's timed launch, committed in
+                 profiles/pmc_summary.json by tools/profile.py), achieved =
                  traffic / the launch's device time measured here (HIP events
-                 on the launch stream); frac = achieved / 8 TB/s.  issue_frac =
-                 the VALU-busy fraction of the same profile (the ceiling that
-                 binds the cache-resident scenes), with the L1/L2 hit rates.
-                 ref_traversal_equiv_GBps restates the rate in SURVEY.md
-                 §8(d)'s B_seg units (bytes the reference's traversal would
-                 move per segment); it is not HBM traffic.
+                 on the launch stream), frac = achieved / 8 TB/s.  On the
+                 cache-resident scenes HBM does not bind: the unit that does,
+                 the vector-memory data path (binding_unit "td"), is reported
+                 in roofline.td -- frac = TD busy cycles per CU per cycle (<= 1),
+                 beside it the busy fraction of the saturating microbenchmark
+                 and the floor of the TD model fitted on every committed
+                 profile (profiles/td_floor_fit.json) -- with the gather fill
+                 of the kernel's own counters (lanes per T-phase node gather,
+                 tests per L phase), issue_frac (VALU busy x lane use) and the
+                 L1/L2 hit rates.  ref_traversal_equiv_GBps restates the rate
+                 in SURVEY.md §8(d)'s B_seg units (bytes the reference's
+                 traversal would move per segment); it is not HBM traffic.
   cpu_baseline — the CPU oracle (plain-C restatement of the reference
                  algorithm, OpenMP on every core this process may use) on a
                  bounded pixel sample of the same workload.
@@ -524,33 +526,44 @@ def main():
                       "gather_latency_cycles_per_vmem_rd", "fetch_scale_calibrated", "timed_launch_ms_rocprof"):
                 roof[k] = prof.get(k)
             roof["profile"] = prof.get("source")
-            # the unit that binds: the vector-memory data path (TD) on the
-            # cache-resident scenes.  Measured: the launch's TD
-            # busy cycles per CU (rocprofv3 TD_TD_BUSY of this command's timed
-            # launch) against the busy fraction of the microbenchmark that
-            # saturates TD with k_render's node-step shape (tools/mb/td_lanes.hip),
-            # so achieved = busy cycles per CU / launch time, peak = the shader
-            # clock x that saturated busy fraction, frac = the launch's share of
-            # what TD sustains.  The modelled floor (the launch's own gather
-            # instructions and line accesses at the microbenchmark's per-
-            # instruction and per-line costs) is beside it.  HBM stays beside
-            # both (roofline.hbm) and is the bound where its fraction is larger.
-            td = prof.get("td_model")
+            # HBM is the roofline the contract names (bound "hbm"); on the
+            # cache-resident scenes the unit that binds is the vector-memory
+            # data path (TD), reported beside it (roofline.td):
+            #   frac       = TD busy cycles per CU per kernel cycle (rocprofv3
+            #                TD_TD_BUSY of this command's timed launch; <= 1 by
+            #                construction), busy_vs_microbench = that over the
+            #                saturating microbenchmark's (tools/mb/td_lanes.hip)
+            #   model_floor_frac = the launch's gather instructions and L2
+            #                requests at the costs fitted on every committed
+            #                profile (profiles/td_floor_fit.json), / its cycles
+            #   fill       = lanes per T-phase node gather (the kernel's own
+            #                counters of the replay: node steps / wave T phases)
+            td, fit = prof.get("td_model"), prof.get("td_fit")
             hbm = {"achieved": roof["achieved"], "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": roof["frac"],
                    "traffic": traffic}
             roof["hbm"] = hbm
             clk = prof.get("clock_GHz")
-            if td and clk and td.get("busy_frac"):
-                sat = td["td_busy_saturated_microbench"]
-                roof["td"] = {"achieved": round(td["td_busy"] * clk, 4), "peak": round(sat * clk, 4),
-                              "unit": "G TD-busy cycles/s per CU", "frac": td["busy_frac"],
-                              "model_floor_frac": td["model_frac"],
-                              "a_cycles_per_gather_inst": td["a_cycles_per_inst"],
-                              "b_cycles_per_line": td["b_cycles_per_line"],
-                              "vmem_rd_insts": td["vmem_rd_insts"], "l1_line_accesses": td["l1_accesses"]}
-                if roof["td"]["frac"] > (hbm["frac"] or 0):
-                    roof.update({"bound": "td", "achieved": roof["td"]["achieved"], "peak": roof["td"]["peak"],
-                                 "unit": roof["td"]["unit"], "frac": roof["td"]["frac"]})
+            if td and clk and fit:
+                roof["binding_unit"] = "td"
+                roof["td"] = {"achieved": round(fit["td_busy_per_cycle"] * clk, 4), "peak": round(clk, 4),
+                              "unit": "G TD-busy cycles/s per CU", "frac": fit["td_busy_per_cycle"],
+                              "busy_vs_microbench": td.get("busy_frac"),
+                              "model_floor_frac": fit["model_frac"], "model": fit["fit"],
+                              "inst_term_share_fitted": fit["inst_term_share"],
+                              "inst_term_share_microbench": round(
+                                  td["a_cycles_per_inst"] * td["vmem_rd_insts"] /
+                                  (td["a_cycles_per_inst"] * td["vmem_rd_insts"] +
+                                   td["b_cycles_per_line"] * td["l1_accesses"]), 4),
+                              "a_cycles_per_gather_inst_microbench": td["a_cycles_per_inst"],
+                              "b_cycles_per_line_microbench": td["b_cycles_per_line"],
+                              "vmem_rd_insts": fit["vmem_rd_insts"], "l1_line_accesses": fit["l1_accesses"],
+                              "l2_requests": fit["l2_requests"],
+                              "l1_lines_per_vmem_rd_inst": fit["l1_lines_per_vmem_rd_inst"]}
+        # gather-instruction fill from the kernel's own counters (the replay):
+        # lanes per T-phase node gather and triangle tests per L phase
+        roof["lanes_per_node_gather_inst"] = round(cst["node_visits"] / max(cst["wave_node_phases"], 1), 2)
+        roof["tests_per_leaf_phase"] = round(cst["tri_tests"] / max(cst["wave_leaf_phases"], 1), 2)
+        roof["helped_node_steps_frac"] = round(cst.get("helped_steps", 0) / max(cst["node_visits"], 1), 4)
         ec = e_counts(args.workload)
         if ec:
             b_seg = 328.0 + 64.0 * (ec["E_node"] + ec["E_tri"])

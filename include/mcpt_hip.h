@@ -176,6 +176,11 @@ typedef struct mcpt_stats {
                                        primary hits; 2: it computed them too  */
   double   primary_ms;              /* primary_cache 2: device time of the
                                        primary-hit pass (part of kernel_ms)   */
+  uint64_t helped_steps;            /* node steps taken by T-phase helpers
+                                       (mcpt_tuning.t_helpers; part of
+                                       node_visits)                           */
+  int32_t  t_helpers;               /* 1: the last call ran with T-phase helpers */
+  int32_t  pad2;
 } mcpt_stats;
 
 /* Launch-plan knobs of the fused kernel (speed only: every setting gives the
@@ -234,6 +239,10 @@ typedef struct mcpt_tuning {
                                consecutive slots are one 8x8 tile), 2 spread
                                (they are one pixel of each of 64 tiles, so one
                                tile's dear pixels run in different waves)      */
+  int32_t t_helpers;        /* EXACT: lanes not stepping in a T phase step their
+                               partner lane's (lane ^ 32) stack-top node with it,
+                               one gather for two nodes of one ray: 0 auto, 1
+                               off, 2 on                                       */
 } mcpt_tuning;
 
 /* ------------------------------------------------------- version / errors */
@@ -488,6 +497,10 @@ int mcpt_gather_probe(mcpt_ctx *ctx, int32_t record_bytes, int64_t table_bytes, 
  * makes: mismatching bit patterns over the 32768 angles 2*pi*r/32768 and
  * over every float in [0, 8). Both counts are 0 on a correct build.       */
 int mcpt_selfcheck_trig(mcpt_ctx *ctx, int64_t *angle_mismatches, int64_t *range_mismatches);
+/* The Phong lobe's pow restatement (cl_pow_lobe, mcpt_refmath.h) against
+ * ocml's pow_f32 over every float of its domain (0, 1 + 2^-10], for each of
+ * the n exponents ys (the scenes' Ns); *mismatches = differing results.      */
+int mcpt_selfcheck_pow(mcpt_ctx *ctx, const float *ys, int32_t n, int64_t *mismatches);
 
 #ifdef __cplusplus
 }

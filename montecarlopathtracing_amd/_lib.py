@@ -51,14 +51,16 @@ class Stats(ctypes.Structure):
                 ("stack_window", ctypes.c_int32), ("workgroups", ctypes.c_int32),
                 ("debug_violations", ctypes.c_uint64), ("phase_ticks", ctypes.c_uint64 * 4),
                 ("leaf_rejects", ctypes.c_uint64), ("quantized", ctypes.c_int32), ("primary_cache", ctypes.c_int32),
-                ("primary_ms", ctypes.c_double)]
+                ("primary_ms", ctypes.c_double), ("helped_steps", ctypes.c_uint64), ("t_helpers", ctypes.c_int32),
+                ("pad2", ctypes.c_int32)]
 
 
 class Tuning(ctypes.Structure):
     """mcpt_tuning: launch-plan knobs of k_render (speed only; 0 = default)."""
     _fields_ = [(n, ctypes.c_int32) for n in (
         "leaf_threshold", "shade_threshold", "queue_chunk", "block_entries", "max_block_frames", "stack_window",
-        "lds_pad", "queues", "fetch_threshold", "quantized", "primary_cache", "last_block_frames", "tile_order", "pixel_spread")]
+        "lds_pad", "queues", "fetch_threshold", "quantized", "primary_cache", "last_block_frames", "tile_order", "pixel_spread",
+        "t_helpers")]
 
 
 class MCPTError(RuntimeError):
@@ -113,6 +115,7 @@ SIGNATURES = {
     "mcpt_get_primary_cost": (_I32, [_P, _P, _I64, _P]),
     "mcpt_get_entry_log": (_I32, [_P, _P, _I64, _P, _P]),
     "mcpt_selfcheck_trig": (_I32, [_P, _P, _P]),
+    "mcpt_selfcheck_pow": (_I32, [_P, _P, _I32, _P]),
     "mcpt_measure_read_bw": (_I32, [_P, _I64, _P]),
     "mcpt_gather_probe": (_I32, [_P, _I32, _I64, _P]),
     "mcpt_build_hlbvh_device": (_I32, [_P, _I64, _P, _P]),

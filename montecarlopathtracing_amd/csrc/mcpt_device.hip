@@ -179,6 +179,7 @@ constexpr int64_t kPrimSmallTree = 1ll << 20;
 // k_render counters (mcpt_stats): kStatSlots words
 constexpr int kPhaseSlot = 16;     // MCPT_PHASE_TIMING: shader-clock ticks per phase (fetch, T, L, S)
 constexpr int kDebugSlot = 12;     // MCPT_DEBUG: violations of the stack bound, node and triangle indices
+constexpr int kHelpSlot = 20;      // STATS: node steps taken by T-phase helpers
 constexpr int kWaveLogWords = 8;   // MCPT_PHASE_TIMING wave log (mcpt_get_wave_log)
 
 // -DMCPT_DEBUG (make debug -> lib/libmcpt_hip_debug.so): k_render checks every
@@ -422,6 +423,48 @@ __device__ inline int32_t step4q(f4 q0, f4 q1, f4 q2, f4 q3, f4 q4, f4 q5, int32
   return nxt;
 }
 
+// step4q's choice without its pushes (k_render's T phase with helpers): the
+// slot to enter and the entries to push, in step4q's push order, so the caller
+// can place them on another lane's stack.
+struct Step4Out {
+  int32_t nxt;         // the slot's link, or kPop
+  int32_t p0, p1, p2;  // entries to push (p0 first); at most 3: one passing slot is entered
+  int32_t n;           // how many
+};
+template <bool PRUNE>
+__device__ inline Step4Out select4q(f4 q0, f4 q1, f4 q2, f4 q3, f4 q4, f4 q5, int32_t l0, int32_t l1, int32_t l2,
+                                    int32_t l3, f3 o, f3 rinv, float tmin, float lim, bool nearest) {
+  BoxT b0 = slab_pairs(q0.xy, q0.zw, q1.xy, o, rinv);
+  BoxT b1 = slab_pairs(q1.zw, q2.xy, q2.zw, o, rinv);
+  BoxT b2 = slab_pairs(q3.xy, q3.zw, q4.xy, o, rinv);
+  BoxT b3 = slab_pairs(q4.zw, q5.xy, q5.zw, o, rinv);
+  bool h0 = slab_pass(b0, tmin) && l0 != kEmptySlot, h1 = slab_pass(b1, tmin) && l1 != kEmptySlot;
+  bool h2 = slab_pass(b2, tmin) && l2 != kEmptySlot, h3 = slab_pass(b3, tmin) && l3 != kEmptySlot;
+  if (PRUNE) {
+    h0 = h0 && !(b0.tnear > lim);
+    h1 = h1 && !(b1.tnear > lim);
+    h2 = h2 && !(b2.tnear > lim);
+    h3 = h3 && !(b3.tnear > lim);
+  }
+  const float k0 = nearest ? b0.tnear : 0.0f, k1 = nearest ? b1.tnear : 0.0f;
+  const float k2 = nearest ? b2.tnear : 0.0f, k3 = nearest ? b3.tnear : 0.0f;
+  Step4Out r;
+  r.nxt = kPop;
+  int sel = 4;
+  float kb = __builtin_inff();
+  if (h3) kb = k3, r.nxt = l3, sel = 3;
+  if (h2 && !(k2 > kb)) kb = k2, r.nxt = l2, sel = 2;
+  if (h1 && !(k1 > kb)) kb = k1, r.nxt = l1, sel = 1;
+  if (h0 && !(k0 > kb)) r.nxt = l0, sel = 0;
+  const bool c3 = h3 && sel != 3, c2 = h2 && sel != 2, c1 = h1 && sel != 1, c0 = h0 && sel != 0;
+  r.p0 = c3 ? l3 : (c2 ? l2 : (c1 ? l1 : l0));
+  r.p1 = c3 ? (c2 ? l2 : (c1 ? l1 : l0)) : (c2 ? (c1 ? l1 : l0) : l0);
+  r.p2 = l0;  // a third push is only ever l0 (c3, c2 and c1 among the first two, or l1 after two of them)
+  r.n = (int32_t)c3 + (int32_t)c2 + (int32_t)c1 + (int32_t)c0;
+  if (r.n == 3 && !c0) r.p2 = l1;  // c3 c2 c1: the third is l1
+  return r;
+}
+
 // Result rule of the EXACT search.  The reference keeps the
 // first triangle in its DFS order and replaces it only by one at least EPS
 // closer (objdef.h:213).  Searching in another order, track the closest
@@ -659,7 +702,7 @@ __device__ inline ShadeOut shade_hit(Mat *__restrict__ mats, const ShadeIn &in, 
       // diffuse: color * kd * cos / 2pi; glossy: color * ks * pow(cos_r, Ns) * cos / 2pi
       f4 c;
       if (lobe)
-        c = color * kaks_of() * cl_pow(cl_dot3(nd.xyz, mir.xyz), Mp->Ns);
+        c = color * kaks_of() * cl_pow_lobe(cl_dot3(nd.xyz, mir.xyz), Mp->Ns);
       else
         c = color * kd_of();
       color = cl_div4(c * cl_dot3(nd.xyz, in.nrm.xyz), (float)(2 * kClPi));
@@ -856,11 +899,12 @@ __device__ inline uint32_t queue_items(uint32_t x, uint32_t n_tiles, uint32_t nq
 // PRIM: the primary-hit pass (PrimHit) run by the same machine: one frame,
 // no pixel state; a lane traces its pixel's primary ray, stores the closest
 // hit at the S phase instead of shading, and takes the next pixel.
-template <int MODE, bool STATS, bool WIN, bool PAIR, bool Q, bool PRIM = false, bool G = true>
+template <int MODE, bool STATS, bool WIN, bool PAIR, bool Q, bool PRIM = false, bool G = true, bool HELP = false>
 __global__ void __launch_bounds__(64, MCPT_WAVES_PER_SIMD) k_render(RenderArgs A) {
   constexpr bool PRUNE = MODE != MCPT_MODE_NOPRUNE;
   constexpr bool LIT = MODE == MCPT_MODE_NOPRUNE;
   static_assert(!(Q && LIT), "the quantized search tree is an EXACT-mode structure");
+  static_assert(!(HELP && (LIT || PRIM)), "T-phase helpers serve the EXACT search only");
   extern __shared__ int32_t lds_stack[];
   const int lane = threadIdx.x;
   // the whole stack in LDS, or its top kStackWindow entries (deep trees, where
@@ -899,7 +943,7 @@ __global__ void __launch_bounds__(64, MCPT_WAVES_PER_SIMD) k_render(RenderArgs A
 
   unsigned long long n_seg = 0, n_nodes = 0, n_tests = 0, n_bad = 0;
   unsigned long long w_t = 0, w_l = 0, w_s = 0, n_fb = 0;
-  unsigned long long w_it = 0, n_wait = 0, n_idle = 0, n_rej = 0;
+  unsigned long long w_it = 0, n_wait = 0, n_idle = 0, n_rej = 0, n_help = 0;
   uint32_t px_seg = 0, px_it = 0;  // STATS: segments / busy iterations of the lane's current entry (A.px_*)
   // pixel state.  lst: this lane's role in the queue protocol, one small
   // int (one VGPR; kept out of lane-mask SGPR pairs on purpose, SGPRs are
@@ -1132,7 +1176,112 @@ __global__ void __launch_bounds__(64, MCPT_WAVES_PER_SIMD) k_render(RenderArgs A
     }
     // ---- T: one node step (objdef.h:252-273 with child boxes)
     const bool in_t = live && cur >= 0;
-    if (__ballot(in_t)) {
+    if constexpr (HELP) {
+      // T-phase helpers: a lane not stepping this iteration
+      // (waiting for L or S, or out of work) steps its partner lane's (lane ^
+      // 32) stack-top node in the same instructions, and pushes what it finds
+      // onto the partner's stack: one gather serves two nodes of one ray, so
+      // the ray's search takes fewer iterations.  EXACT's answer depends only
+      // on the candidate set (pruning with the partner's bound at the time is
+      // safe: it only prunes less than later) and on the order-free t1 / t2
+      // rule; the reference-order search (ref) is never helped.
+      const unsigned long long mt = __ballot(in_t);
+      if (mt) {
+        if (STATS && lane == __builtin_ctzll(__ballot(1))) w_t++;
+        const int partner = lane ^ 32;
+        // offer the stack's top when it is an internal node and the stack has
+        // room for both steps' pushes (the owner's 3, the helper's 3 + 1)
+        int32_t top = -1;
+        if (in_t && !ref && sp > 0 && sp + 6 <= stack_cap) top = stk.peek(sp);
+        const unsigned long long mw = __ballot(top >= 0);
+        const bool give = top >= 0 && !((mt >> partner) & 1ull);
+        const bool help = !in_t && ((mw >> partner) & 1ull);
+        if (give) (void)stk.pop(sp);
+        const float lim_own = best_t + S.prune_margin;
+        int32_t wn = cur;
+        f3 wo = o.xyz, wr = rinv;
+        float wlim = lim_own;
+        if (__ballot(help)) {  // what a helper borrows: the entry, the ray, the pruning bound
+          const int32_t g_n = __shfl_xor(top, 32);
+          const f3 g_o = (f3){__shfl_xor(o.x, 32), __shfl_xor(o.y, 32), __shfl_xor(o.z, 32)};
+          const f3 g_r = (f3){__shfl_xor(rinv.x, 32), __shfl_xor(rinv.y, 32), __shfl_xor(rinv.z, 32)};
+          const float g_lim = __shfl_xor(lim_own, 32);
+          if (help) wn = g_n, wo = g_o, wr = g_r, wlim = g_lim;
+        }
+        const bool act = in_t || help;
+        const bool wref = ref && !help;
+        Step4Out so;
+        so.nxt = kPop, so.p0 = so.p1 = so.p2 = 0, so.n = 0;
+        if (act && MCPT_DCHECK(wn < (wref ? S.n_nodes4 : S.n_near4), 1)) {
+          f4 q0, q1, q2, q3, q4, q5;
+          int32_t l0, l1, l2, l3;
+          if (Q && !wref) {
+            const f4 *p = reinterpret_cast<const f4 *>(S.near4q + wn);
+            const f4 c0 = p[0], c1 = p[1], c2 = p[2], c3 = p[3];
+            const float ox = c0.x, oy = c0.y, oz = c0.z, sx = c0.w, sy = c2.z, sz = c2.w;
+            auto dec = [](uint32_t w, float sa, float oa, float sb, float ob) -> f4 {
+              return (f4){__builtin_fmaf((float)(w & 0xFFu), sa, oa), __builtin_fmaf((float)((w >> 8) & 0xFFu), sa, oa),
+                          __builtin_fmaf((float)((w >> 16) & 0xFFu), sb, ob), __builtin_fmaf((float)(w >> 24), sb, ob)};
+            };
+            q0 = dec(as_u(c1.x), sx, ox, sy, oy);
+            q1 = dec(as_u(c1.y), sz, oz, sx, ox);
+            q2 = dec(as_u(c1.z), sy, oy, sz, oz);
+            q3 = dec(as_u(c1.w), sx, ox, sy, oy);
+            q4 = dec(as_u(c2.x), sz, oz, sx, ox);
+            q5 = dec(as_u(c2.y), sy, oy, sz, oz);
+            l0 = as_i(c3.x), l1 = as_i(c3.y), l2 = as_i(c3.z), l3 = as_i(c3.w);
+          } else {
+            const DevNode4 &N = (wref ? S.nodes4 : S.near4)[wn];
+            q0 = N.q[0], q1 = N.q[1], q2 = N.q[2], q3 = N.q[3], q4 = N.q[4], q5 = N.q[5];
+            l0 = N.link[0], l1 = N.link[1], l2 = N.link[2], l3 = N.link[3];
+          }
+          so = select4q<PRUNE>(q0, q1, q2, q3, q4, q5, l0, l1, l2, l3, wo, wr, kTmin, wlim, !wref);
+          if (STATS) n_nodes++, n_help += help;
+        }
+        // a T lane whose pushes would overflow the stack (helpers' entries can
+        // grow it beyond the single search's bound) restarts the segment as the
+        // reference-order search, from an empty stack: the exact fallback
+        const bool ovf = in_t && !ref && sp + so.n > stack_cap;
+        const int32_t own_end = sp + (in_t && !ovf ? so.n : 0);
+        const int32_t p_end = __shfl_xor(own_end, 32);
+        // pushes: a T lane's onto its own stack, a helper's onto its partner's,
+        // above the partner's own, then the helper's chosen child on top
+        const int32_t np = ovf || !act ? 0 : so.n + (help && so.nxt != kPop ? 1 : 0);
+        const int col = help ? partner : lane;
+        const int32_t base = help ? p_end : sp;
+        for (int k = 0; k < 4; ++k) {
+          if (k < np) {
+            const int32_t v = k == 0 ? (so.n > 0 ? so.p0 : so.nxt)
+                                     : (k == 1 ? (so.n > 1 ? so.p1 : so.nxt) : (k == 2 ? (so.n > 2 ? so.p2 : so.nxt) : so.nxt));
+            const int32_t idx = base + k;
+            if constexpr (WIN) {
+              int32_t *slot = lds_stack + col + (idx & (kStackWindow - 1)) * 64;
+              if (idx >= kStackWindow)
+                A.spill[((size_t)blockIdx.x * 64 + col) * (size_t)A.spill_stride + (idx - kStackWindow)] = *slot;
+              *slot = v;
+            } else {
+              lds_stack[col + idx * 64] = v;
+            }
+          }
+        }
+        const int32_t h_add = __shfl_xor(help ? np : 0, 32);
+        if (in_t) {
+          if (ovf) {
+            if (STATS) n_fb++;
+            ref = true;
+            best_t = kFltMax;
+            t2 = kFltMax;
+            sp = 0;
+            cur = S.root_leaf >= 0 ? ~S.root_leaf : 0;  // the root box passed: the segment was being searched
+          } else {
+            sp = own_end + (give ? h_add : 0);
+            if (!MCPT_DCHECK(sp <= stack_cap, 0)) sp = stack_cap;
+            cur = so.nxt;
+            if (cur == kPop) cur = pop_next();
+          }
+        }
+      }
+    } else if (__ballot(in_t)) {
       if (STATS && lane == __builtin_ctzll(__ballot(1))) w_t++;
       if (in_t) {
         if (Q) {  // EXACT, quantized SAH tree nearest-first (4 loads), or the reference tree left-first
@@ -1435,6 +1584,7 @@ __global__ void __launch_bounds__(64, MCPT_WAVES_PER_SIMD) k_render(RenderArgs A
     if (n_wait) atomicAdd(&A.stats[9], n_wait);
     if (n_idle) atomicAdd(&A.stats[10], n_idle);
     if (n_rej) atomicAdd(&A.stats[11], n_rej);
+    if (n_help) atomicAdd(&A.stats[kHelpSlot], n_help);
   }
 }
 
@@ -1700,6 +1850,37 @@ int mcpt_selfcheck_trig(mcpt_ctx *c, int64_t *angle_bad, int64_t *range_bad) {
   return MCPT_OK;
 }
 
+// cl_pow_lobe vs __ocml_pow_f32, bit for bit, over every float x of the
+// restatement's domain (0, 1 + 2^-10] for each exponent (mcpt_selfcheck_pow)
+__global__ void __launch_bounds__(256) k_selfcheck_pow(const float *ys, int32_t ny, unsigned long long *bad) {
+  constexpr uint32_t kLast = 0x3F802000u;  // 1 + 2^-10
+  unsigned long long n_bad = 0;
+  for (uint32_t b = blockIdx.x * 256u + threadIdx.x + 1u; b <= kLast; b += gridDim.x * 256u) {
+    const float x = __builtin_bit_cast(float, b);
+    for (int k = 0; k < ny; ++k) {
+      const float y = ys[k];
+      n_bad += __builtin_bit_cast(uint32_t, cl_pow_lobe(x, y)) != __builtin_bit_cast(uint32_t, __ocml_pow_f32(x, y));
+    }
+  }
+  if (n_bad) atomicAdd(bad, n_bad);
+}
+
+int mcpt_selfcheck_pow(mcpt_ctx *c, const float *ys, int32_t n, int64_t *mismatches) {
+  if (!c || !ys || n <= 0 || n > 4096 || !mismatches) return mcpt::fail(MCPT_ERR_ARG, "selfcheck_pow: bad argument");
+  HIP_OK(hipSetDevice(c->device));
+  float *dy = nullptr;
+  HIP_OK(hipMalloc(&dy, (size_t)n * sizeof(float)));
+  HIP_OK(hipMemcpy(dy, ys, (size_t)n * sizeof(float), hipMemcpyHostToDevice));
+  HIP_OK(hipMemset(c->d_stats, 0, sizeof(unsigned long long)));
+  hipLaunchKernelGGL(k_selfcheck_pow, dim3((unsigned)(c->n_cu * 16)), dim3(256), 0, 0, dy, n, c->d_stats);
+  HIP_OK(hipGetLastError());
+  unsigned long long h = 0;
+  HIP_OK(hipMemcpy(&h, c->d_stats, sizeof(h), hipMemcpyDeviceToHost));
+  (void)hipFree(dy);
+  *mismatches = (int64_t)h;
+  return MCPT_OK;
+}
+
 // Streaming read of n float4 (grid-stride, 16 B per lane per load), one
 // partial sum per block so nothing is optimised away (mcpt_measure_read_bw).
 __global__ void __launch_bounds__(256) k_stream_read(const f4 *__restrict__ src, int64_t n, float *sink) {
@@ -1851,6 +2032,7 @@ int mcpt_get_stats(mcpt_ctx *c, mcpt_stats *out) {
       c->last.lane_waiting = h[9];
       c->last.lane_idle = h[10];
       c->last.leaf_rejects = h[11];
+      c->last.helped_steps = h[kHelpSlot];
       c->last.debug_violations = h[kDebugSlot] + h[kDebugSlot + 1] + h[kDebugSlot + 2];
       for (int k = 0; k < 4; ++k) c->last.phase_ticks[k] = h[kPhaseSlot + k];
     }
@@ -1888,7 +2070,7 @@ int mcpt_set_tuning(mcpt_ctx *c, const mcpt_tuning *t) {
             t->primary_cache < 0 || t->primary_cache > 2 || t->lds_pad < 0 || t->lds_pad > 65536 ||
             t->queue_chunk > 4096 || t->leaf_threshold > 64 || t->shade_threshold > 64 || t->fetch_threshold > 64 ||
             t->last_block_frames < -1 || t->tile_order < 0 || t->tile_order > 2 || t->pixel_spread < 0 ||
-            t->pixel_spread > 2))
+            t->pixel_spread > 2 || t->t_helpers < 0 || t->t_helpers > 2))
     return mcpt::fail(MCPT_ERR_ARG, "set_tuning: value out of range");
   if (t)
     c->tune = *t;
@@ -2394,14 +2576,15 @@ int mcpt_render_frames(mcpt_ctx *ctx, const mcpt_scene *scene, const mcpt_camera
   // workgroups than a kStackWindow window does, the windowed kernel runs.
   const bool noprune = p->mode == MCPT_MODE_NOPRUNE;
   // [kind: 0 EXACT 128-B nodes, 1 NOPRUNE, 2 EXACT quantized][stats][window][pair]
-  // [kind][stats][window][pair][glossy materials]
-#define MCPT_KG(M, ST, W, P, QN) {(const void *)k_render<M, ST, W, P, QN, false, false>, \
-                                  (const void *)k_render<M, ST, W, P, QN, false, true>}
+  // [glossy materials][T-phase helpers (EXACT only; NOPRUNE's slot is its plain kernel)]
+#define MCPT_KH(M, ST, W, P, QN, GL) {(const void *)k_render<M, ST, W, P, QN, false, GL, false>, \
+                                      (const void *)k_render<M, ST, W, P, QN, false, GL, (M != MCPT_MODE_NOPRUNE)>}
+#define MCPT_KG(M, ST, W, P, QN) {MCPT_KH(M, ST, W, P, QN, false), MCPT_KH(M, ST, W, P, QN, true)}
 #define MCPT_KR(M, ST, W, QN) {MCPT_KG(M, ST, W, false, QN), MCPT_KG(M, ST, W, true, QN)}
 #define MCPT_KK(M, QN) {{MCPT_KR(M, false, false, QN), MCPT_KR(M, false, true, QN)}, \
                         {MCPT_KR(M, true, false, QN), MCPT_KR(M, true, true, QN)}}
-  static const void *const kfns[3][2][2][2][2] = {MCPT_KK(MCPT_MODE_EXACT, false), MCPT_KK(MCPT_MODE_NOPRUNE, false),
-                                                  MCPT_KK(MCPT_MODE_EXACT, true)};
+  static const void *const kfns[3][2][2][2][2][2] = {MCPT_KK(MCPT_MODE_EXACT, false), MCPT_KK(MCPT_MODE_NOPRUNE, false),
+                                                     MCPT_KK(MCPT_MODE_EXACT, true)};
   // the primary-hit pass: [kind][window][pair], no stats
 #define MCPT_KP(M, W, QN) {(const void *)k_render<M, false, W, false, QN, true, false>, \
                            (const void *)k_render<M, false, W, true, QN, true, false>}
@@ -2412,6 +2595,7 @@ int mcpt_render_frames(mcpt_ctx *ctx, const mcpt_scene *scene, const mcpt_camera
 #undef MCPT_KK
 #undef MCPT_KR
 #undef MCPT_KG
+#undef MCPT_KH
   // quantized search tree: forced on (1) or off (2), or auto (0): on when the
   // 128-B tree outgrows the GPU's aggregate L2, where its halved node bytes and
   // gathers pay (C5 -6 %); on cache-resident trees its looser boxes cost more
@@ -2420,6 +2604,8 @@ int mcpt_render_frames(mcpt_ctx *ctx, const mcpt_scene *scene, const mcpt_camera
   const bool quant = scene->near4q && (T.quantized == 1 || (T.quantized == 0 && scene->near4_bytes > kQuantAutoBytes));
   const int kind = noprune ? 1 : (quant ? 2 : 0);
   const int glossy = scene->has_glossy ? 1 : 0;  // the shading instantiation (speed only: same bits)
+  // T-phase helpers (EXACT): forced on (2) or off (1), or auto (0)
+  const int help = !noprune && T.t_helpers == 2 ? 1 : 0;
   const size_t pad = (size_t)std::max(0, T.lds_pad);
   const size_t lds_plain = (size_t)depth_entries * 64 * sizeof(int32_t) + sizeof(LdsUniforms) + lds_mats + pad;
   const size_t lds_win = (size_t)kStackWindow * 64 * sizeof(int32_t) + sizeof(LdsUniforms) + lds_mats + pad;
@@ -2427,22 +2613,22 @@ int mcpt_render_frames(mcpt_ctx *ctx, const mcpt_scene *scene, const mcpt_camera
   int per_cu = 0;
   if (T.stack_window == 1) {  // forced (tests, experiments): the window even when the whole stack fits in it
     win = true;
-    rc = occupancy(ctx, kfns[kind][ctx->stats_on][1][pair][glossy], lds_win, &per_cu);
+    rc = occupancy(ctx, kfns[kind][ctx->stats_on][1][pair][glossy][help], lds_win, &per_cu);
     if (rc) return rc;
   } else if (depth_entries > kStackWindow && T.stack_window != 2) {
     int per_cu_plain = 0, per_cu_win = 0;
-    rc = occupancy(ctx, kfns[kind][ctx->stats_on][0][pair][glossy], lds_plain, &per_cu_plain);
+    rc = occupancy(ctx, kfns[kind][ctx->stats_on][0][pair][glossy][help], lds_plain, &per_cu_plain);
     if (rc) return rc;
-    rc = occupancy(ctx, kfns[kind][ctx->stats_on][1][pair][glossy], lds_win, &per_cu_win);
+    rc = occupancy(ctx, kfns[kind][ctx->stats_on][1][pair][glossy][help], lds_win, &per_cu_win);
     if (rc) return rc;
     win = T.stack_window == 1 || per_cu_win > per_cu_plain;
     per_cu = win ? per_cu_win : per_cu_plain;
   } else {
-    rc = occupancy(ctx, kfns[kind][ctx->stats_on][0][pair][glossy], lds_plain, &per_cu);
+    rc = occupancy(ctx, kfns[kind][ctx->stats_on][0][pair][glossy][help], lds_plain, &per_cu);
     if (rc) return rc;
   }
   const size_t lds = win ? lds_win : lds_plain;
-  const void *kfn = kfns[kind][ctx->stats_on][win][pair][glossy];
+  const void *kfn = kfns[kind][ctx->stats_on][win][pair][glossy][help];
   A.stack_depth = win ? kStackWindow : depth_entries;  // the uniforms and material table follow the stack in LDS
   A.spill_stride = win ? std::max(0, depth_entries - kStackWindow) : 0;
   const int64_t grid = std::max<int64_t>(1, std::min<int64_t>(tiles, (int64_t)std::max(per_cu, 1) * ctx->n_cu));
@@ -2763,6 +2949,7 @@ int mcpt_render_frames(mcpt_ctx *ctx, const mcpt_scene *scene, const mcpt_camera
   ctx->last.frames_per_block = fpl_head;
   ctx->last.stack_window = win ? 1 : 0;
   ctx->last.quantized = kind == 2 ? 1 : 0;
+  ctx->last.t_helpers = help;
   ctx->last.workgroups = (int32_t)grid;
   ctx->last.primary_cache = prim_state;
   ctx->last_pending = true;

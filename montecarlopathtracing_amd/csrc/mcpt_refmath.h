@@ -117,6 +117,31 @@ __device__ inline float cl_length4(f4 p) {
   return cl_sqrt(l2);
 }
 __device__ inline float cl_pow(float x, float y) { return __ocml_pow_f32(x, y); }
+// shade.cl:139's pow(cos_r, Ns) for the ranges the Phong lobe reaches: ocml's
+// pow_f32 (ROCm device libs, gfx950: the fma forms, no unsafe math) is an
+// extended-precision log (__ocmlpriv_epln_f32), y x log in double-float,
+// exp with a correction (__ocmlpriv_expep_f32), then ~40 instructions of
+// special cases (zero, negative, infinite, NaN operands, odd-integer
+// exponents, overflow).  For x in (0, 1 + 2^-10] and y in [0, 65536] none of
+// those cases applies: y x log(x) <= 64 stays finite and below expep's 88.72
+// threshold, exp and the result are finite and >= +0, so ocml returns the
+// core's value unchanged.  The same operations on that domain: the same bits
+// (mcpt_selfcheck_pow compares every float of the domain, for the scenes'
+// exponents, against __ocml_pow_f32); outside it, ocml itself.
+typedef float f2v_ __attribute__((ext_vector_type(2)));
+extern "C" __device__ f2v_ __ocmlpriv_epln_f32(float);
+__device__ inline float cl_pow_lobe(float x, float y) {
+  if (!(x > 0.0f && x <= 0x1.004p0f && y >= 0.0f && y <= 65536.0f)) return __ocml_pow_f32(x, y);
+  const float yy = x == 1.0f ? 1.0f : y;   // ocml: pow(1, y) takes y = 1
+  const float xx = yy == 0.0f ? 1.0f : x;  // and pow(x, 0) takes x = 1
+  const f2v_ e = __ocmlpriv_epln_f32(xx);  // log(xx) as hi (.y) + lo (.x)
+  const float hi = yy * e.y;
+  const float lo = __builtin_fmaf(yy, e.x, __builtin_fmaf(yy, e.y, -hi));
+  const float s = hi + lo;
+  const float rlo = lo - (s - hi);
+  const float ex = __ocml_exp_f32(s);  // expep: exp(hi), then fma(e, lo, e)
+  return __builtin_fmaf(ex, rlo, ex);
+}
 __device__ inline float cl_cos(float x) { return __ocml_cos_f32(x); }
 __device__ inline float cl_sin(float x) { return __ocml_sin_f32(x); }
 __device__ inline float cl_tan(float x) { return __ocml_tan_f32(x); }

@@ -139,7 +139,7 @@ class Renderer:
     def stats(self):
         s = L.Stats()
         L.check(L.lib().mcpt_get_stats(self.ctx, ctypes.byref(s)))
-        out = {f: getattr(s, f) for f, _ in L.Stats._fields_ if f not in ("pad", "pad1")}
+        out = {f: getattr(s, f) for f, _ in L.Stats._fields_ if f not in ("pad", "pad1", "pad2")}
         out["phase_ticks"] = list(out["phase_ticks"])
         return out
 
@@ -218,6 +218,15 @@ class Renderer:
         a, b = ctypes.c_int64(), ctypes.c_int64()
         L.check(L.lib().mcpt_selfcheck_trig(self.ctx, ctypes.byref(a), ctypes.byref(b)))
         return a.value, b.value
+
+    def selfcheck_pow(self, exponents):
+        """Mismatches of the Phong lobe's pow restatement against ocml's
+        pow_f32 over every float in (0, 1 + 2^-10] for each exponent
+        (mcpt_selfcheck_pow); 0 on a good build."""
+        ys = np.ascontiguousarray(exponents, np.float32)
+        n = ctypes.c_int64()
+        L.check(L.lib().mcpt_selfcheck_pow(self.ctx, L.ptr(ys), len(ys), ctypes.byref(n)))
+        return n.value
 
     def measure_read_bw(self, nbytes=4 << 30):
         """Streaming HBM read bandwidth in GB/s (mcpt_measure_read_bw)."""

@@ -63,6 +63,23 @@ def test_tuning_and_params_structs_match_header():
     assert [f for f, _ in L.RenderParams._fields_] == _header_fields(hdr, "mcpt_render_params")
 
 
+def test_abi_struct_sizes_match_header(tmp_path):
+    """The ctypes mirrors of every struct that crosses the ABI have the C
+    compiler's size for the header's definition (mcpt_stats grows at its end
+    too), and the library reports the header's ABI revision."""
+    import subprocess
+    src = tmp_path / "sz.c"
+    src.write_text('#include <stdio.h>\n#include "mcpt_hip.h"\nint main(void) { printf("%zu %zu %zu %d\\n", '
+                   'sizeof(mcpt_stats), sizeof(mcpt_tuning), sizeof(mcpt_render_params), MCPT_ABI_VERSION); '
+                   'return 0; }\n')
+    exe = tmp_path / "sz"
+    subprocess.run(["gcc", "-std=c11", "-I", os.path.join(ROOT, "include"), str(src), "-o", str(exe)], check=True)
+    st, tu, rp, abi = (int(x) for x in subprocess.run([str(exe)], capture_output=True, text=True,
+                                                      check=True).stdout.split())
+    assert (st, tu, rp) == (ctypes.sizeof(L.Stats), ctypes.sizeof(L.Tuning), ctypes.sizeof(L.RenderParams))
+    assert abi == L.ABI_VERSION == L.lib().mcpt_abi_version()
+
+
 def test_record_layouts_match_objdef():
     # objdef.h:21-99 sizes; the C structs are checked by the same numbers in the ABI tests below
     assert (L.CAMERA.itemsize, L.RAY.itemsize, L.HIT.itemsize) == (80, 48, 48)

@@ -86,6 +86,9 @@ def test_bench_default_line():
     assert roof["bound"] == "hbm" and roof["peak"] == 8000.0
     for k in ("frac", "issue_frac", "valu_lane_utilization"):
         assert roof.get(k) is None or 0.0 <= roof[k] <= 1.0, (k, roof.get(k))
+    if "td" in roof:  # the binding unit's busy fraction is a fraction
+        assert 0.0 < roof["td"]["frac"] <= 1.0 and roof["binding_unit"] == "td"
+    assert roof["lanes_per_node_gather_inst"] > 0 and roof["tests_per_leaf_phase"] > 0
     # the primary-hit cache serves each pixel's first segment of each frame
     assert roof["segments_cache_served"] == 1024 * 1024 * 8
     assert roof["segments_traced"] > 0

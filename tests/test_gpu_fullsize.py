@@ -98,7 +98,7 @@ def test_c2_headline_call_bitexact(rnd):
     data, cam, st, seeds, plan = _bench_call(rnd, "C2", 20, 5)
     ref = _ref_render(data, cam, 1024, 1024, 8, 25, seeds)
     _check(st, ref, "C2 bench call %r" % plan)
-    assert (ref[1] > 0).mean() > 0.5  # most pixels saw the light
+    assert (ref[1] > 0).mean() > 0.2  # paths that reached the light (measured 0.29: the box is open to the camera)
 
 
 @needs_ref

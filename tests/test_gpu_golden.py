@@ -36,6 +36,21 @@ def test_inline_sincos_matches_ocml(rnd):
     assert rnd.selfcheck_trig() == (0, 0)
 
 
+def test_lobe_pow_matches_ocml(rnd):
+    """shade.cl:139's pow(cos_r, Ns) restated without ocml's special cases
+    (cl_pow_lobe): every float in (0, 1 + 2^-10] for every glossy exponent of
+    the scenes (cbox, veach_mis, the dining proxy) and edge exponents gives
+    __ocml_pow_f32's bits."""
+    from . import scenes
+    ns = set()
+    for getter in (scenes.cbox, scenes.mis, scenes.dining):
+        m = getter().mats
+        ns |= {float(x) for x in m["Ns"][m["type"] == L.MCPT_GLOSSY]}
+    assert len(ns) >= 4  # veach_mis alone has four plates
+    edges = [0.0, 1e-3, 0.5, 1.0, 2.0, 3.5, 7.25, 50.0, 100.0, 500.0, 4000.0, 65536.0]
+    assert rnd.selfcheck_pow(sorted(ns) + edges) == 0
+
+
 @pytest.mark.parametrize("k", list(CAMS))
 def test_rays_equal_golden(rnd, k):
     mine = R.records(rnd.generate_rays(S.parse_camera(CAMS[k]), 64, 48), L.RAY)

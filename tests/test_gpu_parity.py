@@ -776,3 +776,99 @@ def test_handoff_tag_wrap_bitexact(rnd):
         assert_bits_equal(b.hist.cpu().numpy(), rh, "hist vs reference")
         assert_bits_equal(b.seeds_np(), rs, "seeds vs reference")
     dsc.close()
+
+
+@needs_ref
+@pytest.mark.parametrize("name,getter,camjson,depth", [("cbox", scenes.cbox, scenes.CBOX_CAM, 8),
+                                                       ("cbox_diffuse", scenes.cbox_diffuse, scenes.CBOX_CAM, 8),
+                                                       ("mis", scenes.mis, scenes.MIS_CAM, 12),
+                                                       ("dining", scenes.dining, scenes.DINING_CAM, 16)])
+@pytest.mark.parametrize("quantized", [1, 2])
+@pytest.mark.parametrize("window", [0, 1])
+def test_t_helpers_bitexact(rnd, name, getter, camjson, depth, quantized, window):
+    """T-phase helpers (mcpt_tuning.t_helpers 2): lanes not stepping in a T
+    phase step their partner lane's stack-top node and push onto the
+    partner's stack (its LDS column, or its window and global spill), with
+    the partner's pruning bound.  The candidate set and the order-free
+    t1 / t2 rule are unchanged, so images, counts and seed chains still
+    match the reference kernels bit for bit; the counters show helpers ran."""
+    rnd.set_tuning(t_helpers=2, quantized=quantized, stack_window=window)
+    stats = window == 0 and quantized == 2
+    if stats:
+        rnd.set_stats(True)
+    try:
+        (h_, c_, s_), (rh, rc, rs) = _render_both(rnd, getter(), camjson, 64, 64, depth, 4, 4)
+        st = rnd.stats()
+    finally:
+        rnd.set_stats(False)
+        rnd.set_tuning()
+    assert st["t_helpers"] == 1 and st["stack_window"] == window
+    if stats:
+        assert 0 < st["helped_steps"] < st["node_visits"]
+    assert_bits_equal(c_, rc, "count")
+    assert_bits_equal(s_, rs, "seeds")
+    assert_bits_equal(h_, rh, "hist")
+
+
+@needs_ref
+@pytest.mark.parametrize("name,offset,camjson", NEAR_TIES)
+def test_t_helpers_near_ties_bitexact(rnd, name, offset, camjson):
+    """Helpers with twin triangles less than EPS apart: the ambiguous rays
+    still fall back to the (never helped) reference-order search."""
+    data = scenes.near_ties(name, offset)
+    rnd.set_stats(True)
+    rnd.set_tuning(t_helpers=2)
+    try:
+        (h_, c_, s_), (rh, rc, rs) = _render_both(rnd, data, camjson, 64, 64, 6, 4, 4)
+        st = rnd.stats()
+    finally:
+        rnd.set_stats(False)
+        rnd.set_tuning()
+    assert_bits_equal(c_, rc, "count")
+    assert_bits_equal(s_, rs, "seeds")
+    assert_bits_equal(h_, rh, "hist")
+    assert st["order_fallbacks"] > 0 and st["helped_steps"] > 0
+
+
+@needs_ref
+@pytest.mark.parametrize("quantized", [1, 2])
+def test_t_helpers_random_mesh_bitexact(rnd, quantized):
+    """Helpers on C5's deep random-soup tree (500 K triangles): the deepest
+    stacks, the window stack on auto, 2-frame blocks handed between lanes."""
+    data = _c5_small()
+    rnd.set_tuning(t_helpers=2, quantized=quantized)
+    try:
+        (h_, c_, s_), (rh, rc, rs) = _render_both(rnd, data, S.RANDOM_MESH_CAMERA, 64, 64, 8, 5, 4,
+                                                  frames_per_launch=2)
+        assert rnd.stats()["t_helpers"] == 1
+    finally:
+        rnd.set_tuning()
+    assert_bits_equal(c_, rc, "count")
+    assert_bits_equal(s_, rs, "seeds")
+    assert_bits_equal(h_, rh, "hist")
+
+
+def test_t_helpers_full_size_same_bits(rnd):
+    """Size-independent property at C2's size: helpers on and off give the
+    same image on the whole 1024x1024 image and on a strong-scaled 8-rank
+    share (sparse waves, where most lanes are free to help)."""
+    data, cam = scenes.cbox_diffuse(), S.parse_camera(scenes.CBOX_CAM)
+    w = h = 1024
+    seeds = R.default_seeds(w * h)
+    dsc = rnd.upload(data)
+    try:
+        for stripes in (1, 8):
+            outs = []
+            for th in (1, 2):
+                rnd.set_tuning(t_helpers=th)
+                st = rnd.new_state(w, h, seeds)
+                rnd.render_frames(dsc, cam, st, 8, 1 << 20, 12, stripe_rows=16, stripe_index=stripes - 1,
+                                  stripe_count=stripes)
+                torch.cuda.synchronize()
+                assert rnd.stats()["t_helpers"] == (1 if th == 2 else 0)
+                outs.append((st.hist.cpu().numpy(), st.count.cpu().numpy(), st.seeds_np()))
+            for a, b, what in zip(outs[0], outs[1], ("hist", "count", "seeds")):
+                assert_bits_equal(a, b, "%s / %d stripes" % (what, stripes))
+    finally:
+        rnd.set_tuning()
+        dsc.close()

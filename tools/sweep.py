@@ -134,7 +134,9 @@ def main():
                         "simt_S": round(seg / (64.0 * max(c["wave_shade_phases"], 1)), 3),
                         "waiting_frac": round(c["lane_waiting"] / (64.0 * max(c["wave_iterations"], 1)), 4),
                         "idle_frac": round(c["lane_idle"] / (64.0 * max(c["wave_iterations"], 1)), 4),
-                        "iters_per_seg": round(c["wave_iterations"] * 64.0 / seg, 3)})
+                        "iters_per_seg": round(c["wave_iterations"] * 64.0 / seg, 3),
+                        "helped_frac": round(c.get("helped_steps", 0) / max(c["node_visits"], 1), 4),
+                        "order_fallbacks": c["order_fallbacks"]})
         print(json.dumps(rec), flush=True)
         out.append(rec)
     if a.all_ranks:  # the job: every rank's share at once, as slow as its slowest
