@@ -423,6 +423,41 @@ __device__ inline int32_t step4q(f4 q0, f4 q1, f4 q2, f4 q3, f4 q4, f4 q5, int32
   return nxt;
 }
 
+// The value of lane ^ 32 (k_render's T-phase helpers and their partners).
+// MCPT_HELP_XCHG 1: v_permlane32_swap (gfx950; a VALU swap of the wave's
+// halves, no LDS crossbar); 0: ds_bpermute (__shfl_xor).
+#ifndef MCPT_HELP_XCHG
+#define MCPT_HELP_XCHG 0
+#endif
+__device__ inline uint32_t xor32_u(uint32_t v) {
+#if MCPT_HELP_XCHG == 1
+  // vdst lanes 32-63 <- src lanes 0-31, src lanes 0-31 <- vdst lanes 32-63
+  const auto r = __builtin_amdgcn_permlane32_swap(v, v, true, false);
+  return (threadIdx.x & 32u) ? r[0] : r[1];
+#else
+  return (uint32_t)__shfl_xor((int)v, 32);
+#endif
+}
+__device__ inline int32_t xor32_i(int32_t v) { return (int32_t)xor32_u((uint32_t)v); }
+__device__ inline float xor32_f(float v) { return __builtin_bit_cast(float, xor32_u(__builtin_bit_cast(uint32_t, v))); }
+// MCPT_HELP_PAIRING 1: pairs by rank, the k-th offering lane with the k-th
+// free lane (two ds_permute compactions): 28.5 % of C2's node steps helped,
+// against 14.5 % with 0, partners fixed at lane ^ 32 (profiles/r05_helpers_*).
+#ifndef MCPT_HELP_PAIRING
+#define MCPT_HELP_PAIRING 1
+#endif
+// MCPT_POW_LOBE 0: the Phong lobe calls ocml's pow (A/B builds only)
+#ifndef MCPT_POW_LOBE
+#define MCPT_POW_LOBE 1
+#endif
+__device__ inline uint32_t lane_rank(unsigned long long m) {
+  return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
+__device__ inline int32_t from_lane(int partner, int32_t v) { return __builtin_amdgcn_ds_bpermute(partner << 2, v); }
+__device__ inline float from_lane_f(int partner, float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_ds_bpermute(partner << 2, __builtin_bit_cast(int32_t, v)));
+}
+
 // step4q's choice without its pushes (k_render's T phase with helpers): the
 // slot to enter and the entries to push, in step4q's push order, so the caller
 // can place them on another lane's stack.
@@ -702,7 +737,11 @@ __device__ inline ShadeOut shade_hit(Mat *__restrict__ mats, const ShadeIn &in, 
       // diffuse: color * kd * cos / 2pi; glossy: color * ks * pow(cos_r, Ns) * cos / 2pi
       f4 c;
       if (lobe)
+#if MCPT_POW_LOBE
         c = color * kaks_of() * cl_pow_lobe(cl_dot3(nd.xyz, mir.xyz), Mp->Ns);
+#else
+        c = color * kaks_of() * cl_pow(cl_dot3(nd.xyz, mir.xyz), Mp->Ns);
+#endif
       else
         c = color * kd_of();
       color = cl_div4(c * cl_dot3(nd.xyz, in.nrm.xyz), (float)(2 * kClPi));
@@ -1188,24 +1227,44 @@ __global__ void __launch_bounds__(64, MCPT_WAVES_PER_SIMD) k_render(RenderArgs A
       const unsigned long long mt = __ballot(in_t);
       if (mt) {
         if (STATS && lane == __builtin_ctzll(__ballot(1))) w_t++;
-        const int partner = lane ^ 32;
         // offer the stack's top when it is an internal node and the stack has
         // room for both steps' pushes (the owner's 3, the helper's 3 + 1)
         int32_t top = -1;
         if (in_t && !ref && sp > 0 && sp + 6 <= stack_cap) top = stk.peek(sp);
         const unsigned long long mw = __ballot(top >= 0);
+#if MCPT_HELP_PAIRING == 1
+        // the k-th offering lane with the k-th free lane: every lane sends its
+        // id to its rank's slot (a permutation: others after the listed ones),
+        // then reads its partner's id from the other list
+        const unsigned long long mf = ~mt;
+        const int n_w = __popcll(mw), n_f = __popcll(mf), n_pair = min(n_w, n_f);
+        const bool is_w = top >= 0, is_f = !in_t;
+        const uint32_t r_w = lane_rank(is_w ? mw : ~mw), r_f = lane_rank(is_f ? mf : ~mf);
+        const int32_t wlist = __builtin_amdgcn_ds_permute((int)((is_w ? r_w : n_w + r_w) << 2), lane);
+        const int32_t flist = __builtin_amdgcn_ds_permute((int)((is_f ? r_f : n_f + r_f) << 2), lane);
+        const bool give = is_w && (int)r_w < n_pair;
+        const bool help = is_f && (int)r_f < n_pair;
+        const int32_t h_of_w = from_lane((int)r_w & 63, flist), w_of_f = from_lane((int)r_f & 63, wlist);
+        const int partner = give ? h_of_w : (help ? w_of_f : lane);
+        auto xchg_i = [&](int32_t v) { return from_lane(partner, v); };
+        auto xchg_f = [&](float v) { return from_lane_f(partner, v); };
+#else
+        const int partner = lane ^ 32;
         const bool give = top >= 0 && !((mt >> partner) & 1ull);
         const bool help = !in_t && ((mw >> partner) & 1ull);
+        auto xchg_i = [&](int32_t v) { return xor32_i(v); };
+        auto xchg_f = [&](float v) { return xor32_f(v); };
+#endif
         if (give) (void)stk.pop(sp);
         const float lim_own = best_t + S.prune_margin;
         int32_t wn = cur;
         f3 wo = o.xyz, wr = rinv;
         float wlim = lim_own;
         if (__ballot(help)) {  // what a helper borrows: the entry, the ray, the pruning bound
-          const int32_t g_n = __shfl_xor(top, 32);
-          const f3 g_o = (f3){__shfl_xor(o.x, 32), __shfl_xor(o.y, 32), __shfl_xor(o.z, 32)};
-          const f3 g_r = (f3){__shfl_xor(rinv.x, 32), __shfl_xor(rinv.y, 32), __shfl_xor(rinv.z, 32)};
-          const float g_lim = __shfl_xor(lim_own, 32);
+          const int32_t g_n = xchg_i(top);
+          const f3 g_o = (f3){xchg_f(o.x), xchg_f(o.y), xchg_f(o.z)};
+          const f3 g_r = (f3){xchg_f(rinv.x), xchg_f(rinv.y), xchg_f(rinv.z)};
+          const float g_lim = xchg_f(lim_own);
           if (help) wn = g_n, wo = g_o, wr = g_r, wlim = g_lim;
         }
         const bool act = in_t || help;
@@ -1243,7 +1302,7 @@ __global__ void __launch_bounds__(64, MCPT_WAVES_PER_SIMD) k_render(RenderArgs A
         // reference-order search, from an empty stack: the exact fallback
         const bool ovf = in_t && !ref && sp + so.n > stack_cap;
         const int32_t own_end = sp + (in_t && !ovf ? so.n : 0);
-        const int32_t p_end = __shfl_xor(own_end, 32);
+        const int32_t p_end = xchg_i(own_end);
         // pushes: a T lane's onto its own stack, a helper's onto its partner's,
         // above the partner's own, then the helper's chosen child on top
         const int32_t np = ovf || !act ? 0 : so.n + (help && so.nxt != kPop ? 1 : 0);
@@ -1264,7 +1323,7 @@ __global__ void __launch_bounds__(64, MCPT_WAVES_PER_SIMD) k_render(RenderArgs A
             }
           }
         }
-        const int32_t h_add = __shfl_xor(help ? np : 0, 32);
+        const int32_t h_add = xchg_i(help ? np : 0);
         if (in_t) {
           if (ovf) {
             if (STATS) n_fb++;
