@@ -180,7 +180,7 @@ typedef struct mcpt_stats {
                                        (mcpt_tuning.t_helpers; part of
                                        node_visits)                           */
   int32_t  t_helpers;               /* 1: the last call ran with T-phase helpers */
-  int32_t  pad2;
+  int32_t  merged_gather;           /* 1: the last call ran with merged T / L gathers */
 } mcpt_stats;
 
 /* Launch-plan knobs of the fused kernel (speed only: every setting gives the
@@ -243,6 +243,10 @@ typedef struct mcpt_tuning {
                                partner lane's (lane ^ 32) stack-top node with it,
                                one gather for two nodes of one ray: 0 auto, 1
                                off, 2 on                                       */
+  int32_t merged_gather;    /* EXACT over the 128-B nodes: lanes holding a leaf
+                               fetch their triangles in the T phase's gather
+                               instructions (one gather wait per iteration that
+                               runs both phases): 0 auto, 1 off, 2 on          */
 } mcpt_tuning;
 
 /* ------------------------------------------------------- version / errors */

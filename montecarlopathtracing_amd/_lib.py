@@ -52,7 +52,7 @@ class Stats(ctypes.Structure):
                 ("debug_violations", ctypes.c_uint64), ("phase_ticks", ctypes.c_uint64 * 4),
                 ("leaf_rejects", ctypes.c_uint64), ("quantized", ctypes.c_int32), ("primary_cache", ctypes.c_int32),
                 ("primary_ms", ctypes.c_double), ("helped_steps", ctypes.c_uint64), ("t_helpers", ctypes.c_int32),
-                ("pad2", ctypes.c_int32)]
+                ("merged_gather", ctypes.c_int32)]
 
 
 class Tuning(ctypes.Structure):
@@ -60,7 +60,7 @@ class Tuning(ctypes.Structure):
     _fields_ = [(n, ctypes.c_int32) for n in (
         "leaf_threshold", "shade_threshold", "queue_chunk", "block_entries", "max_block_frames", "stack_window",
         "lds_pad", "queues", "fetch_threshold", "quantized", "primary_cache", "last_block_frames", "tile_order", "pixel_spread",
-        "t_helpers")]
+        "t_helpers", "merged_gather")]
 
 
 class MCPTError(RuntimeError):

@@ -938,12 +938,16 @@ __device__ inline uint32_t queue_items(uint32_t x, uint32_t n_tiles, uint32_t nq
 // PRIM: the primary-hit pass (PrimHit) run by the same machine: one frame,
 // no pixel state; a lane traces its pixel's primary ray, stores the closest
 // hit at the S phase instead of shading, and takes the next pixel.
-template <int MODE, bool STATS, bool WIN, bool PAIR, bool Q, bool PRIM = false, bool G = true, bool HELP = false>
+// VAR: 0 the plain phases, 1 T-phase helpers (t_helpers), 2 merged T / L
+// gathers (merged_gather)
+template <int MODE, bool STATS, bool WIN, bool PAIR, bool Q, bool PRIM = false, bool G = true, int VAR = 0>
 __global__ void __launch_bounds__(64, MCPT_WAVES_PER_SIMD) k_render(RenderArgs A) {
   constexpr bool PRUNE = MODE != MCPT_MODE_NOPRUNE;
   constexpr bool LIT = MODE == MCPT_MODE_NOPRUNE;
+  constexpr bool HELP = VAR == 1, MERGE = VAR == 2;
   static_assert(!(Q && LIT), "the quantized search tree is an EXACT-mode structure");
   static_assert(!(HELP && (LIT || PRIM)), "T-phase helpers serve the EXACT search only");
+  static_assert(!(MERGE && (LIT || PRIM || Q)), "merged gathers: the EXACT search over 128-B nodes");
   extern __shared__ int32_t lds_stack[];
   const int lane = threadIdx.x;
   // the whole stack in LDS, or its top kStackWindow entries (deep trees, where
@@ -1213,6 +1217,50 @@ __global__ void __launch_bounds__(64, MCPT_WAVES_PER_SIMD) k_render(RenderArgs A
       n_wait += lst == kPend;
       n_idle += lst == kNeed || lst == kDead;  // no claim yet, an edge hole, or out of work (tail)
     }
+    // one triangle test with the reference's arithmetic and result rule (the
+    // L phase, and the merged gathers' leaf lanes)
+    using Tri = typename std::conditional<Q, DevTriQ, DevTri>::type;
+    auto test = [&](const Tri &X, int32_t xi) {
+      TriHit h;
+      if constexpr (Q) {
+        // the reference leaf's own box (hlbvh.cpp:97-100: min/max of the
+        // vertices; equal to the stored box, checked at upload), tested with
+        // the reference's arithmetic: the search tree's quantized boxes only
+        // ever let MORE leaves through, this restores exactly its set
+        const f2 bx = (f2){fminf(fminf(X.v0.x, X.v1.x), X.v2.x), fmaxf(fmaxf(X.v0.x, X.v1.x), X.v2.x)};
+        const f2 by = (f2){fminf(fminf(X.v0.y, X.v1.y), X.v2.y), fmaxf(fmaxf(X.v0.y, X.v1.y), X.v2.y)};
+        const f2 bz = (f2){fminf(fminf(X.v0.z, X.v1.z), X.v2.z), fmaxf(fmaxf(X.v0.z, X.v1.z), X.v2.z)};
+        const bool leaf = slab_pass(slab_pairs(bx, by, bz, o.xyz, rinv), kTmin);
+        // objdef.h:190-199: AB = v1 - v0, AC = v2 - v0, matrix rows -AB, -AC
+        const f3 nab = -(X.v1.xyz - X.v0.xyz), nac = -(X.v2.xyz - X.v0.xyz);
+        h = cramer_reduced(d.xyz, nab, nac, X.v0.xyz - o.xyz, X.nrm.xyz, X.v0.w, X.v1.w, X.v2.w, kTmin);
+        h.accept = h.accept && leaf;
+        if (STATS) n_rej += !leaf;
+      } else {
+        const f3 xn = tri_normal(X.v0, X.nab, X.nac);
+        if (LIT) {
+          h = cramer(d.xyz, X.nab.xyz, X.nac.xyz, X.v0.xyz - o.xyz, xn, kTmin);
+        } else {
+          float m_x1, m_y4, m_y8;
+          tri_minors(X.nab.xyz, X.nac.xyz, m_x1, m_y4, m_y8);
+          h = cramer_reduced(d.xyz, X.nab.xyz, X.nac.xyz, X.v0.xyz - o.xyz, xn, m_x1, m_y4, m_y8, kTmin);
+        }
+      }
+      if (STATS) n_tests++;
+      if (h.accept) {
+        if (ref ? best_t - h.t >= kEps : h.t < best_t) {  // objdef.h:213
+          if constexpr (Q)
+            best_nrm = X.nrm;
+          else
+            best_nrm = (f4){X.v0.w, X.nab.w, X.nac.w, as_f(~xi)};  // the material is read at shading
+        }
+        if (ref) {
+          if (best_t - h.t >= kEps) best_t = h.t;
+        } else {
+          near_update(h.t, best_t, t2);
+        }
+      }
+    };
     // ---- T: one node step (objdef.h:252-273 with child boxes)
     const bool in_t = live && cur >= 0;
     if constexpr (HELP) {
@@ -1340,6 +1388,62 @@ __global__ void __launch_bounds__(64, MCPT_WAVES_PER_SIMD) k_render(RenderArgs A
           }
         }
       }
+    } else if constexpr (MERGE) {
+      // Merged gathers: the lanes holding a leaf at the
+      // iteration's start whose L phase runs now (the same threshold rule)
+      // fetch their triangles in the T phase's load instructions -- each
+      // gather takes a node for a T lane and a triangle (or the paired two)
+      // for an L lane -- so an iteration that runs both phases waits for one
+      // gather, and the L phase's own gather instructions disappear.  A lane
+      // whose T step ends on a leaf tests it next iteration; its sequence of
+      // operations is unchanged, and so are the bits.
+      const unsigned long long mt = __ballot(in_t);
+      const bool in_l0 = live && cur < 0 && cur != kDone;
+      const unsigned long long ml0 = __ballot(in_l0);
+      const bool run_l = ml0 && (__popcll(ml0) >= th_leaf || !mt);
+      if (mt || run_l) {
+        if (STATS && lane == __builtin_ctzll(__ballot(1))) {
+          if (mt) w_t++;
+          if (run_l) w_l++;
+        }
+        const bool gl = run_l && in_l0;
+        const int32_t nx = (PAIR && gl && sp > 0) ? stk.peek(sp) : kDone;
+        const bool two = PAIR && gl && nx < 0 && nx != kDone;
+        const int32_t ti = gl && MCPT_DCHECK(~cur < S.n_tris, 2) ? ~cur : 0;
+        const int32_t ti2 = two && MCPT_DCHECK(~nx < S.n_tris, 2) ? ~nx : 0;
+        const DevNode4 *__restrict__ tree = ref ? S.nodes4 : S.near4;
+        const bool node_ok = in_t && MCPT_DCHECK(cur < (ref ? S.n_nodes4 : S.n_near4), 1);
+        const f4 *a = in_t ? reinterpret_cast<const f4 *>(tree + (node_ok ? cur : 0))
+                           : reinterpret_cast<const f4 *>(S.tris + ti);
+        const f4 *b = in_t ? a + 3 : reinterpret_cast<const f4 *>(S.tris + ti2);
+        f4 g0 = (f4){0.0f, 0.0f, 0.0f, 0.0f}, g1 = g0, g2 = g0, g3 = g0, g4 = g0, g5 = g0, g6 = g0;
+        if (in_t || gl) g0 = a[0], g1 = a[1], g2 = a[2];  // node planes 0-2, or the triangle's 48 B
+        if (in_t || two) g3 = b[0], g4 = b[1], g5 = b[2];  // node planes 3-5, or the paired triangle
+        if (in_t) g6 = a[6];                              // node links
+        if (in_t) {
+          uint32_t ctr = 0;
+          if (node_ok) {
+            cur = step4q<PRUNE>(g0, g1, g2, g3, g4, g5, as_i(g6.x), as_i(g6.y), as_i(g6.z), as_i(g6.w), o.xyz, rinv,
+                                kTmin, best_t + S.prune_margin, !ref, stk, sp, ctr);
+            if (!MCPT_DCHECK(sp <= stack_cap, 0)) sp = stack_cap;
+          } else {
+            cur = kPop;
+          }
+          if (STATS) n_nodes += ctr;
+          if (cur == kPop) cur = pop_next();
+        }
+        if (gl) {
+          Tri X{};
+          X.v0 = g0, X.nab = g1, X.nac = g2;
+          test(X, ti);
+          if (two) {
+            (void)stk.pop(sp);
+            X.v0 = g3, X.nab = g4, X.nac = g5;
+            test(X, ti2);
+          }
+          cur = pop_next();
+        }
+      }
     } else if (__ballot(in_t)) {
       if (STATS && lane == __builtin_ctzll(__ballot(1))) w_t++;
       if (in_t) {
@@ -1422,10 +1526,10 @@ __global__ void __launch_bounds__(64, MCPT_WAVES_PER_SIMD) k_render(RenderArgs A
       }
     }
     MCPT_TICK(1);
-    // ---- L: triangle tests, batched
-    const bool in_l = live && cur < 0 && cur != kDone;
+    // ---- L: triangle tests, batched (MERGE: run with the T phase's gathers)
+    const bool in_l = !MERGE && live && cur < 0 && cur != kDone;
     const unsigned long long ml = __ballot(in_l);
-    if (ml && (__popcll(ml) >= th_leaf || !__ballot(live && cur >= 0))) {
+    if (!MERGE && ml && (__popcll(ml) >= th_leaf || !__ballot(live && cur >= 0))) {
       if (STATS && lane == __builtin_ctzll(__ballot(1))) w_l++;
       if (in_l) {
         // PAIR (MCPT_SCHED_PAIRED): when the next stack entry is a leaf too,
@@ -1433,7 +1537,6 @@ __global__ void __launch_bounds__(64, MCPT_WAVES_PER_SIMD) k_render(RenderArgs A
         // the lane's sequence of tests is unchanged, one phase serves two leaves
         const int32_t nx = !PAIR || sp == 0 ? kDone : stk.peek(sp);
         const bool two = PAIR && nx < 0 && nx != kDone;
-        using Tri = typename std::conditional<Q, DevTriQ, DevTri>::type;
         const Tri *tri_arr;
         if constexpr (Q)
           tri_arr = S.triq;
@@ -1447,47 +1550,6 @@ __global__ void __launch_bounds__(64, MCPT_WAVES_PER_SIMD) k_render(RenderArgs A
           ti2 = MCPT_DCHECK(~nx < S.n_tris, 2) ? ~nx : 0;
           T2 = tri_arr[ti2];
         }
-        auto test = [&](const Tri &X, int32_t xi) {
-          TriHit h;
-          if constexpr (Q) {
-            // the reference leaf's own box (hlbvh.cpp:97-100: min/max of the
-            // vertices; equal to the stored box, checked at upload), tested with
-            // the reference's arithmetic: the search tree's quantized boxes only
-            // ever let MORE leaves through, this restores exactly its set
-            const f2 bx = (f2){fminf(fminf(X.v0.x, X.v1.x), X.v2.x), fmaxf(fmaxf(X.v0.x, X.v1.x), X.v2.x)};
-            const f2 by = (f2){fminf(fminf(X.v0.y, X.v1.y), X.v2.y), fmaxf(fmaxf(X.v0.y, X.v1.y), X.v2.y)};
-            const f2 bz = (f2){fminf(fminf(X.v0.z, X.v1.z), X.v2.z), fmaxf(fmaxf(X.v0.z, X.v1.z), X.v2.z)};
-            const bool leaf = slab_pass(slab_pairs(bx, by, bz, o.xyz, rinv), kTmin);
-            // objdef.h:190-199: AB = v1 - v0, AC = v2 - v0, matrix rows -AB, -AC
-            const f3 nab = -(X.v1.xyz - X.v0.xyz), nac = -(X.v2.xyz - X.v0.xyz);
-            h = cramer_reduced(d.xyz, nab, nac, X.v0.xyz - o.xyz, X.nrm.xyz, X.v0.w, X.v1.w, X.v2.w, kTmin);
-            h.accept = h.accept && leaf;
-            if (STATS) n_rej += !leaf;
-          } else {
-            const f3 xn = tri_normal(X.v0, X.nab, X.nac);
-            if (LIT) {
-              h = cramer(d.xyz, X.nab.xyz, X.nac.xyz, X.v0.xyz - o.xyz, xn, kTmin);
-            } else {
-              float m_x1, m_y4, m_y8;
-              tri_minors(X.nab.xyz, X.nac.xyz, m_x1, m_y4, m_y8);
-              h = cramer_reduced(d.xyz, X.nab.xyz, X.nac.xyz, X.v0.xyz - o.xyz, xn, m_x1, m_y4, m_y8, kTmin);
-            }
-          }
-          if (STATS) n_tests++;
-          if (h.accept) {
-            if (ref ? best_t - h.t >= kEps : h.t < best_t) {  // objdef.h:213
-              if constexpr (Q)
-                best_nrm = X.nrm;
-              else
-                best_nrm = (f4){X.v0.w, X.nab.w, X.nac.w, as_f(~xi)};  // the material is read at shading
-            }
-            if (ref) {
-              if (best_t - h.t >= kEps) best_t = h.t;
-            } else {
-              near_update(h.t, best_t, t2);
-            }
-          }
-        };
         test(T, ti);
         if (two) {
           (void)stk.pop(sp);
@@ -2129,7 +2191,8 @@ int mcpt_set_tuning(mcpt_ctx *c, const mcpt_tuning *t) {
             t->primary_cache < 0 || t->primary_cache > 2 || t->lds_pad < 0 || t->lds_pad > 65536 ||
             t->queue_chunk > 4096 || t->leaf_threshold > 64 || t->shade_threshold > 64 || t->fetch_threshold > 64 ||
             t->last_block_frames < -1 || t->tile_order < 0 || t->tile_order > 2 || t->pixel_spread < 0 ||
-            t->pixel_spread > 2 || t->t_helpers < 0 || t->t_helpers > 2))
+            t->pixel_spread > 2 || t->t_helpers < 0 || t->t_helpers > 2 || t->merged_gather < 0 ||
+            t->merged_gather > 2))
     return mcpt::fail(MCPT_ERR_ARG, "set_tuning: value out of range");
   if (t)
     c->tune = *t;
@@ -2635,14 +2698,16 @@ int mcpt_render_frames(mcpt_ctx *ctx, const mcpt_scene *scene, const mcpt_camera
   // workgroups than a kStackWindow window does, the windowed kernel runs.
   const bool noprune = p->mode == MCPT_MODE_NOPRUNE;
   // [kind: 0 EXACT 128-B nodes, 1 NOPRUNE, 2 EXACT quantized][stats][window][pair]
-  // [glossy materials][T-phase helpers (EXACT only; NOPRUNE's slot is its plain kernel)]
-#define MCPT_KH(M, ST, W, P, QN, GL) {(const void *)k_render<M, ST, W, P, QN, false, GL, false>, \
-                                      (const void *)k_render<M, ST, W, P, QN, false, GL, (M != MCPT_MODE_NOPRUNE)>}
+  // [glossy materials][variant: plain, T-phase helpers (EXACT), merged gathers
+  // (EXACT, 128-B nodes); a slot a kind does not have holds its plain kernel]
+#define MCPT_KH(M, ST, W, P, QN, GL) {(const void *)k_render<M, ST, W, P, QN, false, GL, 0>, \
+                                      (const void *)k_render<M, ST, W, P, QN, false, GL, (M != MCPT_MODE_NOPRUNE) ? 1 : 0>, \
+                                      (const void *)k_render<M, ST, W, P, QN, false, GL, (M != MCPT_MODE_NOPRUNE && !QN) ? 2 : 0>}
 #define MCPT_KG(M, ST, W, P, QN) {MCPT_KH(M, ST, W, P, QN, false), MCPT_KH(M, ST, W, P, QN, true)}
 #define MCPT_KR(M, ST, W, QN) {MCPT_KG(M, ST, W, false, QN), MCPT_KG(M, ST, W, true, QN)}
 #define MCPT_KK(M, QN) {{MCPT_KR(M, false, false, QN), MCPT_KR(M, false, true, QN)}, \
                         {MCPT_KR(M, true, false, QN), MCPT_KR(M, true, true, QN)}}
-  static const void *const kfns[3][2][2][2][2][2] = {MCPT_KK(MCPT_MODE_EXACT, false), MCPT_KK(MCPT_MODE_NOPRUNE, false),
+  static const void *const kfns[3][2][2][2][2][3] = {MCPT_KK(MCPT_MODE_EXACT, false), MCPT_KK(MCPT_MODE_NOPRUNE, false),
                                                      MCPT_KK(MCPT_MODE_EXACT, true)};
   // the primary-hit pass: [kind][window][pair], no stats
 #define MCPT_KP(M, W, QN) {(const void *)k_render<M, false, W, false, QN, true, false>, \
@@ -2663,8 +2728,9 @@ int mcpt_render_frames(mcpt_ctx *ctx, const mcpt_scene *scene, const mcpt_camera
   const bool quant = scene->near4q && (T.quantized == 1 || (T.quantized == 0 && scene->near4_bytes > kQuantAutoBytes));
   const int kind = noprune ? 1 : (quant ? 2 : 0);
   const int glossy = scene->has_glossy ? 1 : 0;  // the shading instantiation (speed only: same bits)
-  // T-phase helpers (EXACT): forced on (2) or off (1), or auto (0)
-  const int help = !noprune && T.t_helpers == 2 ? 1 : 0;
+  // the kernel's variant: T-phase helpers (EXACT; t_helpers 2) or merged
+  // T / L gathers (EXACT over the 128-B nodes; merged_gather 2); auto (0): plain
+  const int help = !noprune && T.t_helpers == 2 ? 1 : (!noprune && !quant && T.merged_gather == 2 ? 2 : 0);
   const size_t pad = (size_t)std::max(0, T.lds_pad);
   const size_t lds_plain = (size_t)depth_entries * 64 * sizeof(int32_t) + sizeof(LdsUniforms) + lds_mats + pad;
   const size_t lds_win = (size_t)kStackWindow * 64 * sizeof(int32_t) + sizeof(LdsUniforms) + lds_mats + pad;
@@ -3008,7 +3074,8 @@ int mcpt_render_frames(mcpt_ctx *ctx, const mcpt_scene *scene, const mcpt_camera
   ctx->last.frames_per_block = fpl_head;
   ctx->last.stack_window = win ? 1 : 0;
   ctx->last.quantized = kind == 2 ? 1 : 0;
-  ctx->last.t_helpers = help;
+  ctx->last.t_helpers = help == 1 ? 1 : 0;
+  ctx->last.merged_gather = help == 2 ? 1 : 0;
   ctx->last.workgroups = (int32_t)grid;
   ctx->last.primary_cache = prim_state;
   ctx->last_pending = true;

@@ -139,7 +139,7 @@ class Renderer:
     def stats(self):
         s = L.Stats()
         L.check(L.lib().mcpt_get_stats(self.ctx, ctypes.byref(s)))
-        out = {f: getattr(s, f) for f, _ in L.Stats._fields_ if f not in ("pad", "pad1", "pad2")}
+        out = {f: getattr(s, f) for f, _ in L.Stats._fields_ if f not in ("pad", "pad1")}
         out["phase_ticks"] = list(out["phase_ticks"])
         return out
 

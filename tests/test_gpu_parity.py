@@ -872,3 +872,87 @@ def test_t_helpers_full_size_same_bits(rnd):
     finally:
         rnd.set_tuning()
         dsc.close()
+
+
+@needs_ref
+@pytest.mark.parametrize("name,getter,camjson,depth", [("cbox", scenes.cbox, scenes.CBOX_CAM, 8),
+                                                       ("cbox_diffuse", scenes.cbox_diffuse, scenes.CBOX_CAM, 8),
+                                                       ("mis", scenes.mis, scenes.MIS_CAM, 12),
+                                                       ("dining", scenes.dining, scenes.DINING_CAM, 16)])
+@pytest.mark.parametrize("schedule", [L.SCHED_SINGLE, L.SCHED_PAIRED])
+@pytest.mark.parametrize("window", [2, 1])
+def test_merged_gather_bitexact(rnd, name, getter, camjson, depth, schedule, window):
+    """Merged T / L gathers (mcpt_tuning.merged_gather 2, the 128-B search
+    tree): a lane holding a leaf at the iteration's start fetches its
+    triangle (or the paired two) in the T phase's load instructions, and a
+    T step that ends on a leaf is tested next iteration.  Every lane's
+    sequence of operations is the same, so images, counts and seed chains
+    match the reference kernels bit for bit, with either leaf schedule and
+    stack layout, counters on and off."""
+    rnd.set_tuning(merged_gather=2, quantized=2, stack_window=window)
+    stats = window == 2
+    if stats:
+        rnd.set_stats(True)
+    try:
+        (h_, c_, s_), (rh, rc, rs) = _render_both(rnd, getter(), camjson, 64, 64, depth, 4, 4, schedule=schedule)
+        st = rnd.stats()
+    finally:
+        rnd.set_stats(False)
+        rnd.set_tuning()
+    assert st["merged_gather"] == 1 and st["quantized"] == 0 and st["stack_window"] == (1 if window == 1 else 0)
+    if stats:
+        assert st["tri_tests"] > 0 and st["wave_leaf_phases"] > 0
+    assert_bits_equal(c_, rc, "count")
+    assert_bits_equal(s_, rs, "seeds")
+    assert_bits_equal(h_, rh, "hist")
+
+
+@needs_ref
+@pytest.mark.parametrize("name,offset,camjson", NEAR_TIES)
+def test_merged_gather_near_ties_bitexact(rnd, name, offset, camjson):
+    """Merged gathers with twin triangles less than EPS apart: the
+    reference-order fallback runs through the merged phase too."""
+    data = scenes.near_ties(name, offset)
+    rnd.set_stats(True)
+    rnd.set_tuning(merged_gather=2, quantized=2)
+    try:
+        (h_, c_, s_), (rh, rc, rs) = _render_both(rnd, data, camjson, 64, 64, 6, 4, 4)
+        st = rnd.stats()
+    finally:
+        rnd.set_stats(False)
+        rnd.set_tuning()
+    assert_bits_equal(c_, rc, "count")
+    assert_bits_equal(s_, rs, "seeds")
+    assert_bits_equal(h_, rh, "hist")
+    assert st["order_fallbacks"] > 0 and st["merged_gather"] == 1
+
+
+def test_merged_gather_full_size_same_bits(rnd):
+    """Size-independent property at C2's and C4's sizes: merged gathers on
+    and off give the same image on the whole image and on an 8-rank share;
+    the quantized tree (C5's) keeps the plain phases."""
+    for getter, camjson, depth, w, h, frames in ((scenes.cbox_diffuse, scenes.CBOX_CAM, 8, 1024, 1024, 12),
+                                                 (scenes.dining, scenes.DINING_CAM, 16, 1920, 1080, 3)):
+        data, cam = getter(), S.parse_camera(camjson)
+        seeds = R.default_seeds(w * h)
+        dsc = rnd.upload(data)
+        try:
+            for stripes in (1, 8):
+                outs = []
+                for mg in (1, 2):
+                    rnd.set_tuning(merged_gather=mg)
+                    st = rnd.new_state(w, h, seeds)
+                    rnd.render_frames(dsc, cam, st, depth, 1 << 20, frames, stripe_rows=16, stripe_index=stripes - 1,
+                                      stripe_count=stripes)
+                    torch.cuda.synchronize()
+                    assert rnd.stats()["merged_gather"] == (1 if mg == 2 else 0)
+                    outs.append((st.hist.cpu().numpy(), st.count.cpu().numpy(), st.seeds_np()))
+                for a, b, what in zip(outs[0], outs[1], ("hist", "count", "seeds")):
+                    assert_bits_equal(a, b, "%s / %d stripes" % (what, stripes))
+            rnd.set_tuning(merged_gather=2, quantized=1)
+            st = rnd.new_state(64, 64)
+            rnd.render_frames(dsc, cam, st, depth, 4, 1)
+            assert rnd.stats()["merged_gather"] == 0 and rnd.stats()["quantized"] == 1
+        finally:
+            rnd.set_tuning()
+            dsc.close()

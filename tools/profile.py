@@ -153,7 +153,8 @@ def summarize(tag):
     sched = bench["config"]["schedule"]
     quant = "true" if bench["config"].get("search_tree_nodes", "").startswith("64") else "false"
     # the render instantiation (PRIM = false), not the primary-hit pass (PRIM = true)
-    kname = r"k_render<0, false, (false|true), %s, %s, false, (false|true)>" % ("true" if sched == "paired" else "false", quant)
+    kname = r"k_render<0, false, (false|true), %s, %s, false, (false|true)(, [a-z0-9]+)?>" % (
+        "true" if sched == "paired" else "false", quant)
     trace = [r for r in csv.DictReader(open(trace_csv)) if re.search(kname, r["Kernel_Name"])]
     timed = trace[-1]
     timed_ms = (int(timed["End_Timestamp"]) - int(timed["Start_Timestamp"])) / 1e6

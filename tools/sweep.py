@@ -30,7 +30,7 @@ from montecarlopathtracing_amd import scene as S  # noqa: E402
 
 def parse_grid(text):
     axes = []
-    for part in (text or "").split():
+    for part in (text or "").replace("+", " ").split():  # axes separated by spaces or '+
         k, vals = part.split("=")
         axes.append([(k, int(v)) for v in vals.split(",")])
     return [dict(c) for c in itertools.product(*axes)] if axes else [{}]

@@ -28,7 +28,7 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 PROF = os.path.join(ROOT, "profiles")
 RENDER_KERNELS = re.compile(r"k_render|k_primary|k_tile_")
-NON_PRIM = re.compile(r"k_render<[^>]*, false, (false|true)>")
+NON_PRIM = re.compile(r"k_render<[^>]*, false, (false|true)(, [a-z0-9]+)?>")
 
 
 def _rows(text):
