@@ -159,3 +159,36 @@ def test_c5_full_tree_bitexact(rnd):
     for quantized, _, st in outs:
         _check(st, ref, "C5 full tree (quantized=%d)" % quantized)
     assert (ref[1] > 0).any()
+
+
+@needs_ref
+@pytest.mark.parametrize("workload,frames,rank", [("C2", 20, 3), ("C4", 4, 6)])
+def test_strong_share_full_size_bitexact(rnd, workload, frames, rank):
+    """One rank's share of an 8-GPU strong-scaled job at the config's own
+    size (16-row stripes dealt round-robin; the auto plan spreads each
+    wave's pixel slots over 64 tiles at these ~0.5-1 pixels per resident lane
+    and runs one or two blocks per pixel): the rows the rank owns equal the
+    reference kernels' full image bit for bit, and the rows it does not own
+    stay untouched (zero)."""
+    from montecarlopathtracing_amd import dist as D
+    wl = bench.WORKLOADS[workload]
+    w, h, depth = wl["w"], wl["h"], wl["depth"]
+    data, camj = bench.load_scene(workload)
+    cam = S.parse_camera(camj)
+    dsc, _ = bench.upload_scene(rnd, data)
+    seeds = bench.default_seeds(w * h)
+    try:
+        st = rnd.new_state(w, h, seeds)
+        rnd.render_frames(dsc, cam, st, depth, bench.ATTEMPT, frames, stripe_rows=bench.STRIPE_ROWS,
+                          stripe_index=rank, stripe_count=8)
+        torch.cuda.synchronize()
+    finally:
+        dsc.close()
+    rh, rc, rs = _ref_render(data, cam, w, h, depth, frames, seeds)
+    own = D.ownership_mask(w, h, bench.STRIPE_ROWS, rank, 8)
+    hist, count, sd = st.hist.cpu().numpy(), st.count.cpu().numpy(), st.seeds_np()
+    _bits_equal(count[own], rc[own], "%s share count" % workload)
+    _bits_equal(sd[own], rs[own], "%s share seeds" % workload)
+    _bits_equal(hist[own], rh[own], "%s share hist" % workload)
+    assert not hist[~own].any() and not count[~own].any()
+    assert (sd[~own] == seeds[~own]).all()
