@@ -17,6 +17,9 @@
 
 #include "mcpt_bvh4.h"
 
+#ifndef MCPT_SAH_BINS  // centroid bins per axis (A/B builds only: mcpt_upload.hip's GPU build uses 32 too)
+#define MCPT_SAH_BINS 32
+#endif
 #ifndef MCPT_COLLAPSE_CTRI  // cost of a triangle test per node step in the collapse (A/B builds only)
 #define MCPT_COLLAPSE_CTRI 1.7
 #endif
@@ -56,7 +59,7 @@ struct Builder {
 
   // returns the split position in idx (lo < mid < hi)
   int64_t split(int64_t lo, int64_t hi) {
-    constexpr int NB = 32;
+    constexpr int NB = MCPT_SAH_BINS;
     float cmin[3] = {FLT_MAX, FLT_MAX, FLT_MAX}, cmax[3] = {-FLT_MAX, -FLT_MAX, -FLT_MAX};
     for (int64_t i = lo; i < hi; ++i) {
       const float *c = &cen[3 * (size_t)idx[i]];
