@@ -192,3 +192,20 @@ def test_strong_share_full_size_bitexact(rnd, workload, frames, rank):
     _bits_equal(hist[own], rh[own], "%s share hist" % workload)
     assert not hist[~own].any() and not count[~own].any()
     assert (sd[~own] == seeds[~own]).all()
+
+
+@needs_ref
+def test_c5_full_size_image_bitexact(rnd):
+    """C5 at its own image size: 2048x2048, depth 8, over the whole 10 M-
+    triangle GPU-treelet tree, through bench.py's own scene load, device build
+    and plan tuning, 1 warmup + 1 timed frame: bit-identical to the reference
+    kernels (whose exhaustive traversal of the soup is the slow side here)."""
+    data, cam, st, seeds, plan = _bench_call(rnd, "C5", 1, 1)
+    dt = R.to_device(data.tris, 0)
+    dn = R.build_hlbvh_device(dt)
+    R.treelet_gpu_device(dn)
+    nodes = R.records(dn, L.BVHNODE).copy()
+    del dt, dn
+    ref = _ref_render(data.with_nodes(nodes), cam, 2048, 2048, 8, 2, seeds)
+    _check(st, ref, "C5 2048^2 %r" % plan)
+    assert (ref[1] > 0).any()
