@@ -777,3 +777,61 @@ def test_spread_slot_mapping_is_a_bijection(n_tiles):
             assert sorted(got) == [(u, k) for u in range(n_q) for k in range(64)]
             if n_q >= 64:
                 assert len({u for u, _ in got[:64]}) == 64
+
+
+def test_trim_profiles_keeps_the_timed_dispatch(tmp_path):
+    """tools/trim_profiles.py: a --pmc pass keeps only the rows of the timed
+    dispatch (the last dispatch of the kernel its summary names), a trace only
+    the render path's kernels; what tools/profile.py summarises is unchanged."""
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("trim", os.path.join(ROOT, "tools", "trim_profiles.py"))
+    T = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(T)
+    k = "void k_render<0, false, false, true, false, false, false, 0>(RenderArgs)"
+    kp = "void k_render<0, false, false, true, false, true, false, 0>(RenderArgs)"
+    hdr = '"Dispatch_Id","Kernel_Name","Counter_Name","Counter_Value"\n'
+    rows = [(1, "__amd_rocclr_fillBufferAligned", "SQ_WAVES", 4), (2, kp, "SQ_WAVES", 10), (3, k, "SQ_WAVES", 20),
+            (3, k, "GRBM_GUI_ACTIVE", 30), (4, kp, "SQ_WAVES", 11), (5, k, "SQ_WAVES", 40), (5, k, "GRBM_GUI_ACTIVE", 50)]
+    pmc = tmp_path / "rx_pmc_sq.csv"
+    pmc.write_text(hdr + "".join('%d,"%s","%s",%d\n' % r for r in rows))
+    (tmp_path / "rx_summary.json").write_text(json.dumps({"kernel": k}))
+    trace = tmp_path / "rx_kernel_trace.csv"
+    trace.write_text('"Dispatch_Id","Kernel_Name"\n1,"__amd_rocclr_copyBuffer"\n2,"%s"\n3,"k_tile_sort(x)"\n' % k)
+    T.main([str(pmc), str(trace)])
+    import csv
+    kept = list(csv.DictReader(open(pmc)))
+    assert [(int(r["Dispatch_Id"]), r["Counter_Name"], float(r["Counter_Value"])) for r in kept] == \
+        [(5, "SQ_WAVES", 40.0), (5, "GRBM_GUI_ACTIVE", 50.0)]
+    assert [r["Kernel_Name"] for r in csv.DictReader(open(trace))] == [k, "k_tile_sort(x)"]
+
+
+def test_td_floor_fit_is_recomputable():
+    """profiles/td_floor_fit.json is what tools/profile.py refit computes from
+    the committed summaries, and the bench line's TD fields stay fractions:
+    every pmc_summary.json entry's TD busy per cycle is at most 1."""
+    fit = json.load(open(os.path.join(ROOT, "profiles", "td_floor_fit.json")))
+    assert fit["profiles"] >= 35 and fit["a_cycles_per_gather_inst"] > 0 and fit["c_cycles_per_l2_request"] > 0
+    for wl, (lo, hi) in fit["range_by_workload"].items():
+        assert 0.7 < lo <= hi < 1.1, (wl, lo, hi)
+    entries = json.load(open(os.path.join(ROOT, "profiles", "pmc_summary.json")))
+    for key, e in entries.items():
+        summ = json.load(open(os.path.join(ROOT, e["source"])))
+        c = summ["counters_timed_dispatch"]
+        busy = c["TD_TD_BUSY_sum"] / (summ.get("cus", 256) * summ["kernel_cycles"])
+        assert abs(busy - e["td_fit"]["td_busy_per_cycle"]) < 1e-3 and busy <= 1.0, key
+        floor = (fit["a_cycles_per_gather_inst"] * c["SQ_INSTS_VMEM_RD"] + fit["b_cycles_per_l1_hit_line"] *
+                 (c["TCP_TOTAL_CACHE_ACCESSES_sum"] - c["TCP_TCC_READ_REQ_sum"]) +
+                 fit["c_cycles_per_l2_request"] * c["TCP_TCC_READ_REQ_sum"]) / summ.get("cus", 256)
+        assert abs(floor / summ["kernel_cycles"] - e["td_fit"]["model_frac"]) < 2e-3, key
+
+
+def test_bench_strong_record():
+    """bench.strong_record: the striped rate, every rank's share time, and the
+    speed-up over the same image rendered on one GPU inside the job."""
+    import bench
+    bench.DEPTH = 8
+    r = bench.strong_record(1024, 1024, 20, 0.004, [0.003, 0.004], 0.0092, "n")
+    assert r["value"] == round(1024 * 1024 * 20 * 8 / 0.004 / 1e6, 2)
+    assert r["share_ms_per_rank"] == [3.0, 4.0] and r["share_max_over_mean"] == round(4 / 3.5, 4)
+    assert r["one_gpu_ms"] == 9.2 and r["speedup_vs_1gpu"] == 2.3
+    assert bench.strong_record(8, 8, 1, 1.0, [1.0], None, "n")["speedup_vs_1gpu"] is None
