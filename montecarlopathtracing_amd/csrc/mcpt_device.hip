@@ -372,6 +372,36 @@ struct WindowStack {
   }
   __device__ inline int32_t peek(int sp) const { return lds[((sp - 1) & (K - 1)) * 64]; }  // the top is in the window
 };
+// The same logical stack with its top entry held in a register (k_render,
+// MCPT_TOPREG): entries [0, sp-1) in the inner stack, entry sp-1 in `top`.
+// A pop returns the register at once and refills it from the inner stack,
+// so the LDS read is off the path of the step that uses the popped entry;
+// a peek costs nothing.  A push writes the old top, as the inner push would.
+#ifndef MCPT_TOPREG
+#define MCPT_TOPREG 0
+#endif
+template <class Inner>
+struct TopStack {
+  const Inner &in;
+  int32_t &top;
+  __device__ inline void push(int &sp, int32_t v) const {
+    if (sp > 0) {
+      int t = sp - 1;
+      in.push(t, top);
+    }
+    top = v;
+    ++sp;
+  }
+  __device__ inline int32_t pop(int &sp) const {
+    const int32_t v = top;
+    if (--sp > 0) {
+      int t = sp;
+      top = in.pop(t);
+    }
+    return v;
+  }
+  __device__ inline int32_t peek(int) const { return top; }
+};
 
 // One 4-wide node: slab test of the 4 slots, then pick the slot to enter.
 // NEAREST (the SAH search tree): the passing slot with the smallest entry
@@ -1015,7 +1045,17 @@ __global__ void __launch_bounds__(64, MCPT_WAVES_PER_SIMD) k_render(RenderArgs A
   // traverse_exact); t2 = runner-up t of the nearest-first search
   bool ref = LIT;
   float t2 = kFltMax;
-  auto pop_next = [&]() -> int32_t { return sp == 0 ? kDone : stk.pop(sp); };
+  // the stack the phases use: the LDS stack, or (TOPREG, plain phases only)
+  // the same stack with its top in a register
+  constexpr bool TOPREG = MCPT_TOPREG && VAR == 0;
+  int32_t tos = 0;
+  const auto sk = [&] {
+    if constexpr (TOPREG)
+      return TopStack<Stack>{stk, tos};
+    else
+      return stk;
+  }();
+  auto pop_next = [&]() -> int32_t { return sp == 0 ? kDone : sk.pop(sp); };
   auto begin_segment = [&]() {
     rinv.x = __builtin_amdgcn_rcpf(d.x);
     rinv.y = __builtin_amdgcn_rcpf(d.y);
@@ -1278,7 +1318,7 @@ __global__ void __launch_bounds__(64, MCPT_WAVES_PER_SIMD) k_render(RenderArgs A
         // offer the stack's top when it is an internal node and the stack has
         // room for both steps' pushes (the owner's 3, the helper's 3 + 1)
         int32_t top = -1;
-        if (in_t && !ref && sp > 0 && sp + 6 <= stack_cap) top = stk.peek(sp);
+        if (in_t && !ref && sp > 0 && sp + 6 <= stack_cap) top = sk.peek(sp);
         const unsigned long long mw = __ballot(top >= 0);
 #if MCPT_HELP_PAIRING == 1
         // the k-th offering lane with the k-th free lane: every lane sends its
@@ -1303,7 +1343,7 @@ __global__ void __launch_bounds__(64, MCPT_WAVES_PER_SIMD) k_render(RenderArgs A
         auto xchg_i = [&](int32_t v) { return xor32_i(v); };
         auto xchg_f = [&](float v) { return xor32_f(v); };
 #endif
-        if (give) (void)stk.pop(sp);
+        if (give) (void)sk.pop(sp);
         const float lim_own = best_t + S.prune_margin;
         int32_t wn = cur;
         f3 wo = o.xyz, wr = rinv;
@@ -1407,7 +1447,7 @@ __global__ void __launch_bounds__(64, MCPT_WAVES_PER_SIMD) k_render(RenderArgs A
           if (run_l) w_l++;
         }
         const bool gl = run_l && in_l0;
-        const int32_t nx = (PAIR && gl && sp > 0) ? stk.peek(sp) : kDone;
+        const int32_t nx = (PAIR && gl && sp > 0) ? sk.peek(sp) : kDone;
         const bool two = PAIR && gl && nx < 0 && nx != kDone;
         const int32_t ti = gl && MCPT_DCHECK(~cur < S.n_tris, 2) ? ~cur : 0;
         const int32_t ti2 = two && MCPT_DCHECK(~nx < S.n_tris, 2) ? ~nx : 0;
@@ -1424,7 +1464,7 @@ __global__ void __launch_bounds__(64, MCPT_WAVES_PER_SIMD) k_render(RenderArgs A
           uint32_t ctr = 0;
           if (node_ok) {
             cur = step4q<PRUNE>(g0, g1, g2, g3, g4, g5, as_i(g6.x), as_i(g6.y), as_i(g6.z), as_i(g6.w), o.xyz, rinv,
-                                kTmin, best_t + S.prune_margin, !ref, stk, sp, ctr);
+                                kTmin, best_t + S.prune_margin, !ref, sk, sp, ctr);
             if (!MCPT_DCHECK(sp <= stack_cap, 0)) sp = stack_cap;
           } else {
             cur = kPop;
@@ -1437,7 +1477,7 @@ __global__ void __launch_bounds__(64, MCPT_WAVES_PER_SIMD) k_render(RenderArgs A
           X.v0 = g0, X.nab = g1, X.nac = g2;
           test(X, ti);
           if (two) {
-            (void)stk.pop(sp);
+            (void)sk.pop(sp);
             X.v0 = g3, X.nab = g4, X.nac = g5;
             test(X, ti2);
           }
@@ -1474,7 +1514,7 @@ __global__ void __launch_bounds__(64, MCPT_WAVES_PER_SIMD) k_render(RenderArgs A
               l0 = N.link[0], l1 = N.link[1], l2 = N.link[2], l3 = N.link[3];
             }
             cur = step4q<PRUNE>(q0, q1, q2, q3, q4, q5, l0, l1, l2, l3, o.xyz, rinv, kTmin, best_t + S.prune_margin,
-                                !ref, stk, sp, ctr);
+                                !ref, sk, sp, ctr);
             if (!MCPT_DCHECK(sp <= stack_cap, 0)) sp = stack_cap;
           } else {
             cur = kPop;
@@ -1491,7 +1531,7 @@ __global__ void __launch_bounds__(64, MCPT_WAVES_PER_SIMD) k_render(RenderArgs A
 #elif MCPT_PROBE == 4  // one more 16-B load per node step, the same address in every lane
             const f4 pad = tree[0].pad;
 #endif
-            cur = step4<PRUNE>(tree[cur], o.xyz, rinv, kTmin, best_t + S.prune_margin, !ref, stk, sp, ctr);
+            cur = step4<PRUNE>(tree[cur], o.xyz, rinv, kTmin, best_t + S.prune_margin, !ref, sk, sp, ctr);
 #if MCPT_PROBE == 1 || MCPT_PROBE == 3 || MCPT_PROBE == 4
             if (__builtin_expect(as_i(pad.x) == 0x7FC0DEAD, 0)) cur = kPop;
 #elif MCPT_PROBE == 2  // sensitivity probe (not shipped): 16 more VALU per node step
@@ -1518,7 +1558,7 @@ __global__ void __launch_bounds__(64, MCPT_WAVES_PER_SIMD) k_render(RenderArgs A
             hl = hl && !(bl.tnear > lim);
             hr = hr && !(br.tnear > lim);
           }
-          if (hl && hr) stk.push(sp, N.right);  // push right, descend left
+          if (hl && hr) sk.push(sp, N.right);  // push right, descend left
           cur = hl ? N.left : (hr ? N.right : kPop);
           if (!MCPT_DCHECK(sp <= stack_cap, 0)) sp = stack_cap;
         }
@@ -1535,7 +1575,7 @@ __global__ void __launch_bounds__(64, MCPT_WAVES_PER_SIMD) k_render(RenderArgs A
         // PAIR (MCPT_SCHED_PAIRED): when the next stack entry is a leaf too,
         // its triangle is fetched with this one and tested right after it;
         // the lane's sequence of tests is unchanged, one phase serves two leaves
-        const int32_t nx = !PAIR || sp == 0 ? kDone : stk.peek(sp);
+        const int32_t nx = !PAIR || sp == 0 ? kDone : sk.peek(sp);
         const bool two = PAIR && nx < 0 && nx != kDone;
         const Tri *tri_arr;
         if constexpr (Q)
@@ -1552,7 +1592,7 @@ __global__ void __launch_bounds__(64, MCPT_WAVES_PER_SIMD) k_render(RenderArgs A
         }
         test(T, ti);
         if (two) {
-          (void)stk.pop(sp);
+          (void)sk.pop(sp);
           test(T2, ti2);
         }
         cur = pop_next();
