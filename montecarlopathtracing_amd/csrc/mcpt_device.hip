@@ -46,6 +46,13 @@ using namespace mcpt;
 #ifndef MCPT_STACK_WINDOW_K
 #define MCPT_STACK_WINDOW_K 32
 #endif
+#ifndef MCPT_COOP  // cooperative node gathers in k_render's T phase (A/B builds)
+#define MCPT_COOP 0
+#endif
+#ifndef MCPT_COOP_ROUNDS  // their gathers per node step at most (9 nodes each)
+#define MCPT_COOP_ROUNDS 8
+#endif
+constexpr int kLdsPerCu = 160 * 1024;  // gfx950
 constexpr int kStackWindow = MCPT_STACK_WINDOW_K;  // k_render's LDS window when the whole stack would cost occupancy
 
 namespace mcpt {
@@ -930,6 +937,8 @@ struct RenderArgs {
   const int32_t *tile_order;  // queue position -> 8x8 tile (dearest first, mcpt_tuning.tile_order), or nullptr: image order
   uint32_t *entry_log;        // MCPT_PHASE_TIMING: per (pixel, block) claim / start / end times (mcpt_get_entry_log), or nullptr
   int32_t spread;             // 1: each run of 64 queue slots takes one pixel from each of 64 tiles (mcpt_tuning.pixel_spread)
+  int32_t coop_off;           // COOP: byte offset of the node staging in LDS
+  int32_t coop_nmax;          // COOP: nodes the staging holds
 };
 
 __device__ inline int32_t global_row(int32_t lr, const RenderArgs &A) {
@@ -1048,6 +1057,7 @@ __global__ void __launch_bounds__(64, MCPT_WAVES_PER_SIMD) k_render(RenderArgs A
   // the stack the phases use: the LDS stack, or (TOPREG, plain phases only)
   // the same stack with its top in a register
   constexpr bool TOPREG = MCPT_TOPREG && VAR == 0;
+  constexpr bool COOP = MCPT_COOP && VAR == 0 && !LIT && !Q && !PRIM;
   int32_t tos = 0;
   const auto sk = [&] {
     if constexpr (TOPREG)
@@ -1486,6 +1496,61 @@ __global__ void __launch_bounds__(64, MCPT_WAVES_PER_SIMD) k_render(RenderArgs A
       }
     } else if (__ballot(in_t)) {
       if (STATS && lane == __builtin_ctzll(__ballot(1))) w_t++;
+      // COOP (cooperative node gathers): the wave fetches its T lanes' nodes
+      // seven lanes to a node, one 16-B chunk each, nine nodes per
+      // instruction, into an LDS staging area (MCPT_COOP 1: global_load_lds;
+      // 2: into registers, then ds_write); each T lane then reads its node
+      // from LDS.  An instruction touches 9 lines instead of one per T lane,
+      // and a node step issues ceil(T lanes / 9) gathers instead of 7.  T
+      // lanes ranked past the staging area (A.coop_nmax nodes) gather their
+      // own node as before.  Same nodes, same bits.
+      bool staged = false;
+      const f4 *cgp = nullptr;  // COOP: this lane's staged node in LDS
+      if constexpr (COOP) {
+        const unsigned long long mt = __ballot(in_t);
+        const int nt = __popcll(mt);
+        const int nst = nt < A.coop_nmax ? nt : A.coop_nmax;
+        const bool node_ok = in_t && MCPT_DCHECK(cur < (ref ? S.n_nodes4 : S.n_near4), 1);
+        const uint32_t rk_t = lane_rank(mt);
+        // a permutation of the lanes: T lanes to their rank, the others after them
+        const uint32_t rk = in_t ? rk_t : (uint32_t)nt + lane_rank(~mt);
+        const int32_t gid = node_ok ? (ref ? S.n_near4 + cur : cur) : -1;
+        const int32_t byrank = __builtin_amdgcn_ds_permute((int)(rk << 2), gid);  // lane j: rank j's node
+        const int grp = lane / 7, ch = lane - 7 * grp;
+        char *const stage = reinterpret_cast<char *>(lds_stack) + A.coop_off;
+        constexpr int R = MCPT_COOP_ROUNDS;  // rounds: up to 9 R nodes staged (A.coop_nmax <= 9 R)
+        int32_t gk[R];
+#pragma unroll
+        for (int k = 0; k < R; ++k)  // every round's node id first: one LDS wait, not one per round
+          gk[k] = 9 * k < nst ? __builtin_amdgcn_ds_bpermute(((9 * k + grp) & 63) << 2, byrank) : -1;
+        auto chunk = [&](int k) -> const f4 * {
+          const int32_t g = gk[k];
+          const DevNode4 *nb = g < S.n_near4 ? S.near4 + g : S.nodes4 + (g - S.n_near4);
+          return reinterpret_cast<const f4 *>(nb) + ch;
+        };
+        if constexpr (MCPT_COOP == 1) {
+          typedef __attribute__((address_space(3))) void LdsVoid;
+#pragma unroll
+          for (int k = 0; k < R; ++k)
+            if (9 * k < nst && grp < 9 && 9 * k + grp < nst && gk[k] >= 0)
+              __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void *)chunk(k),
+                                               (LdsVoid *)(stage + k * 9 * 112), 16, 0, 0);
+          __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): the staged nodes are in LDS (hipcc does not count LDS-DMA)
+          __asm__ __volatile__("" ::: "memory");
+        } else {
+          typedef __attribute__((address_space(3))) f4 LdsF4w;
+          f4 v[R];
+#pragma unroll
+          for (int k = 0; k < R; ++k)
+            if (9 * k < nst && grp < 9 && 9 * k + grp < nst && gk[k] >= 0) v[k] = *chunk(k);
+#pragma unroll
+          for (int k = 0; k < R; ++k)
+            if (9 * k < nst && grp < 9 && 9 * k + grp < nst && gk[k] >= 0)
+              *(LdsF4w *)(stage + k * 9 * 112 + lane * 16) = v[k];
+        }
+        staged = in_t && (int)rk_t < nst && node_ok;
+        cgp = reinterpret_cast<const f4 *>(stage + rk_t * 112);
+      }
       if (in_t) {
         if (Q) {  // EXACT, quantized SAH tree nearest-first (4 loads), or the reference tree left-first
           uint32_t ctr = 0;
@@ -1531,7 +1596,21 @@ __global__ void __launch_bounds__(64, MCPT_WAVES_PER_SIMD) k_render(RenderArgs A
 #elif MCPT_PROBE == 4  // one more 16-B load per node step, the same address in every lane
             const f4 pad = tree[0].pad;
 #endif
-            cur = step4<PRUNE>(tree[cur], o.xyz, rinv, kTmin, best_t + S.prune_margin, !ref, sk, sp, ctr);
+            if constexpr (COOP) {  // the staged node (LDS-typed reads: ds_read_b128), or an overflow lane's own
+              typedef const __attribute__((address_space(3))) f4 LdsF4;
+              f4 c0, c1, c2, c3, c4, c5, c6;
+              if (staged) {
+                LdsF4 *q = (LdsF4 *)cgp;
+                c0 = q[0], c1 = q[1], c2 = q[2], c3 = q[3], c4 = q[4], c5 = q[5], c6 = q[6];
+              } else {
+                const f4 *q = reinterpret_cast<const f4 *>(tree + cur);
+                c0 = q[0], c1 = q[1], c2 = q[2], c3 = q[3], c4 = q[4], c5 = q[5], c6 = q[6];
+              }
+              cur = step4q<PRUNE>(c0, c1, c2, c3, c4, c5, as_i(c6.x), as_i(c6.y), as_i(c6.z), as_i(c6.w), o.xyz, rinv,
+                                  kTmin, best_t + S.prune_margin, !ref, sk, sp, ctr);
+            } else {
+              cur = step4<PRUNE>(tree[cur], o.xyz, rinv, kTmin, best_t + S.prune_margin, !ref, sk, sp, ctr);
+            }
 #if MCPT_PROBE == 1 || MCPT_PROBE == 3 || MCPT_PROBE == 4
             if (__builtin_expect(as_i(pad.x) == 0x7FC0DEAD, 0)) cur = kPop;
 #elif MCPT_PROBE == 2  // sensitivity probe (not shipped): 16 more VALU per node step
@@ -2772,8 +2851,21 @@ int mcpt_render_frames(mcpt_ctx *ctx, const mcpt_scene *scene, const mcpt_camera
   // T / L gathers (EXACT over the 128-B nodes; merged_gather 2); auto (0): plain
   const int help = !noprune && T.t_helpers == 2 ? 1 : (!noprune && !quant && T.merged_gather == 2 ? 2 : 0);
   const size_t pad = (size_t)std::max(0, T.lds_pad);
-  const size_t lds_plain = (size_t)depth_entries * 64 * sizeof(int32_t) + sizeof(LdsUniforms) + lds_mats + pad;
-  const size_t lds_win = (size_t)kStackWindow * 64 * sizeof(int32_t) + sizeof(LdsUniforms) + lds_mats + pad;
+  // COOP builds (MCPT_COOP): the cooperative node gathers' LDS staging follows
+  // the uniforms and the material table, as many 112-B nodes as the LDS
+  // leaves per wave at the kernel's occupancy target (at least one gather's 9)
+  const bool coop = MCPT_COOP && kind == 0 && help == 0;
+  const size_t base_plain = ((size_t)depth_entries * 64 * sizeof(int32_t) + sizeof(LdsUniforms) + lds_mats + 15) & ~(size_t)15;
+  const size_t base_win = ((size_t)kStackWindow * 64 * sizeof(int32_t) + sizeof(LdsUniforms) + lds_mats + 15) & ~(size_t)15;
+  auto coop_nodes = [&](size_t base) -> int {
+    if (!coop) return 0;
+    const size_t budget = (size_t)kLdsPerCu / (4 * MCPT_WAVES_PER_SIMD);
+    if (base + pad + 9 * 112 > budget) return 9;
+    return (int)std::min<size_t>(std::min(64, 9 * MCPT_COOP_ROUNDS), (budget - base - pad) / 112);
+  };
+  const int coop_plain = coop_nodes(base_plain), coop_win = coop_nodes(base_win);
+  const size_t lds_plain = base_plain + (size_t)coop_plain * 112 + pad;
+  const size_t lds_win = base_win + (size_t)coop_win * 112 + pad;
   bool win = false;
   int per_cu = 0;
   if (T.stack_window == 1) {  // forced (tests, experiments): the window even when the whole stack fits in it
@@ -2786,7 +2878,8 @@ int mcpt_render_frames(mcpt_ctx *ctx, const mcpt_scene *scene, const mcpt_camera
     if (rc) return rc;
     rc = occupancy(ctx, kfns[kind][ctx->stats_on][1][pair][glossy][help], lds_win, &per_cu_win);
     if (rc) return rc;
-    win = T.stack_window == 1 || per_cu_win > per_cu_plain;
+    // COOP: at equal occupancy the window, whose smaller stack leaves more staging
+    win = T.stack_window == 1 || per_cu_win > per_cu_plain || (coop && per_cu_win == per_cu_plain);
     per_cu = win ? per_cu_win : per_cu_plain;
   } else {
     rc = occupancy(ctx, kfns[kind][ctx->stats_on][0][pair][glossy][help], lds_plain, &per_cu);
@@ -2796,6 +2889,8 @@ int mcpt_render_frames(mcpt_ctx *ctx, const mcpt_scene *scene, const mcpt_camera
   const void *kfn = kfns[kind][ctx->stats_on][win][pair][glossy][help];
   A.stack_depth = win ? kStackWindow : depth_entries;  // the uniforms and material table follow the stack in LDS
   A.spill_stride = win ? std::max(0, depth_entries - kStackWindow) : 0;
+  A.coop_off = (int32_t)(win ? base_win : base_plain);
+  A.coop_nmax = win ? coop_win : coop_plain;
   const int64_t grid = std::max<int64_t>(1, std::min<int64_t>(tiles, (int64_t)std::max(per_cu, 1) * ctx->n_cu));
   const int64_t spill_need = win ? grid * 64 * (int64_t)A.spill_stride : 0;
   if (win && spill_need > ctx->spill_cap) {
