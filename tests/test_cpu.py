@@ -835,3 +835,21 @@ def test_bench_strong_record():
     assert r["share_ms_per_rank"] == [3.0, 4.0] and r["share_max_over_mean"] == round(4 / 3.5, 4)
     assert r["one_gpu_ms"] == 9.2 and r["speedup_vs_1gpu"] == 2.3
     assert bench.strong_record(8, 8, 1, 1.0, [1.0], None, "n")["speedup_vs_1gpu"] is None
+
+
+def test_variant_names_map_to_macros(tmp_path):
+    """`make variants` (the A/B builds tools/ab.py and tools/sweep.py time):
+    each letter of a variant name sets its macro, the rest keep the shipped
+    values (dry run: the compiler is `echo`)."""
+    import subprocess
+    out = subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "montecarlopathtracing_amd", "csrc"), "variants",
+                          "VARIANTS=w4k16c1g6 w5r1", "HIPCC=echo", "OUT=%s" % tmp_path],
+                         capture_output=True, text=True, check=True).stdout
+    lines = [ln for ln in out.splitlines() if "mcpt_device.hip" in ln]
+    assert len(lines) == 2
+    macros = [dict(re.findall(r"-D(MCPT_[A-Z_]+)=(\S+)", ln)) for ln in lines]
+    assert macros[0] == {"MCPT_WAVES_PER_SIMD": "4", "MCPT_STACK_WINDOW_K": "16", "MCPT_PROBE": "0",
+                         "MCPT_HELP_XCHG": "0", "MCPT_HELP_PAIRING": "1", "MCPT_POW_LOBE": "1", "MCPT_TOPREG": "0",
+                         "MCPT_COOP": "1", "MCPT_COOP_ROUNDS": "6"}
+    assert macros[1]["MCPT_WAVES_PER_SIMD"] == "5" and macros[1]["MCPT_TOPREG"] == "1"
+    assert macros[1]["MCPT_COOP"] == "0" and macros[1]["MCPT_STACK_WINDOW_K"] == "32"
