@@ -176,11 +176,8 @@ typedef struct mcpt_stats {
                                        primary hits; 2: it computed them too  */
   double   primary_ms;              /* primary_cache 2: device time of the
                                        primary-hit pass (part of kernel_ms)   */
-  uint64_t helped_steps;            /* node steps taken by T-phase helpers
-                                       (mcpt_tuning.t_helpers; part of
-                                       node_visits)                           */
-  int32_t  t_helpers;               /* 1: the last call ran with T-phase helpers */
-  int32_t  merged_gather;           /* 1: the last call ran with merged T / L gathers */
+  int32_t  wide_nodes;              /* 1: the last call searched the 8-wide
+                                       search tree (EXACT mode)               */
 } mcpt_stats;
 
 /* Launch-plan knobs of the fused kernel (speed only: every setting gives the
@@ -239,23 +236,23 @@ typedef struct mcpt_tuning {
                                consecutive slots are one 8x8 tile), 2 spread
                                (they are one pixel of each of 64 tiles, so one
                                tile's dear pixels run in different waves)      */
-  int32_t t_helpers;        /* EXACT: lanes not stepping in a T phase step their
-                               partner lane's (lane ^ 32) stack-top node with it,
-                               one gather for two nodes of one ray: 0 auto, 1
-                               off, 2 on                                       */
-  int32_t merged_gather;    /* EXACT over the 128-B nodes: lanes holding a leaf
-                               fetch their triangles in the T phase's gather
-                               instructions (one gather wait per iteration that
-                               runs both phases): 0 auto, 1 off, 2 on          */
+  int32_t wide_nodes;       /* EXACT search tree width: 0 auto (the 4-wide
+                               tree), 1 the 4-wide tree (128-B or quantized
+                               nodes, `quantized`), 2 the 8-wide tree (256-B
+                               nodes, fewer dependent node steps per ray;
+                               DESIGN.md §3.3)                                  */
 } mcpt_tuning;
 
 /* ------------------------------------------------------- version / errors */
 /* The ABI revision this header describes.  It changes whenever a struct
- * passed across the boundary changes size or an entry point its arguments
- * (3: mcpt_tuning's tile_order / pixel_spread, mcpt_set_pixel_segments'
- * capacity).  A binding checks mcpt_abi_version() == MCPT_ABI_VERSION once
- * at load and refuses a library built from another header.               */
-#define MCPT_ABI_VERSION 3
+ * passed across the boundary changes size or layout, or an entry point its
+ * arguments (3: mcpt_tuning's tile_order / pixel_spread,
+ * mcpt_set_pixel_segments' capacity; 4: the rejected T-phase-helper and
+ * merged-gather knobs and counters removed from mcpt_tuning / mcpt_stats,
+ * `wide_nodes` added to both).  A binding checks mcpt_abi_version() ==
+ * MCPT_ABI_VERSION once at load and refuses a library built from another
+ * header.                                                                */
+#define MCPT_ABI_VERSION 4
 int32_t mcpt_abi_version(void);
 const char *mcpt_version(void);
 const char *mcpt_last_error(void);

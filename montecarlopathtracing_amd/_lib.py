@@ -28,7 +28,7 @@ BVHNODE = np.dtype([("bbmin", "<f4", 4), ("bbmax", "<f4", 4), ("pad", "<f4", 4),
 for _dt, _sz in ((CAMERA, 80), (RAY, 48), (HIT, 48), (TRIANGLE, 64), (MATERIAL, 48), (BVHNODE, 64)):
     assert _dt.itemsize == _sz
 
-ABI_VERSION = 3  # include/mcpt_hip.h MCPT_ABI_VERSION
+ABI_VERSION = 4  # include/mcpt_hip.h MCPT_ABI_VERSION
 MCPT_DIFFUSE, MCPT_GLOSSY, MCPT_TRANSPARENT, MCPT_LIGHT = 1, 2, 3, 4
 MODE_EXACT, MODE_NOPRUNE = 0, 1
 SCHED_SINGLE, SCHED_PAIRED = 0, 1  # mcpt_render_params.schedule
@@ -51,8 +51,7 @@ class Stats(ctypes.Structure):
                 ("stack_window", ctypes.c_int32), ("workgroups", ctypes.c_int32),
                 ("debug_violations", ctypes.c_uint64), ("phase_ticks", ctypes.c_uint64 * 4),
                 ("leaf_rejects", ctypes.c_uint64), ("quantized", ctypes.c_int32), ("primary_cache", ctypes.c_int32),
-                ("primary_ms", ctypes.c_double), ("helped_steps", ctypes.c_uint64), ("t_helpers", ctypes.c_int32),
-                ("merged_gather", ctypes.c_int32)]
+                ("primary_ms", ctypes.c_double), ("wide_nodes", ctypes.c_int32)]
 
 
 class Tuning(ctypes.Structure):
@@ -60,7 +59,7 @@ class Tuning(ctypes.Structure):
     _fields_ = [(n, ctypes.c_int32) for n in (
         "leaf_threshold", "shade_threshold", "queue_chunk", "block_entries", "max_block_frames", "stack_window",
         "lds_pad", "queues", "fetch_threshold", "quantized", "primary_cache", "last_block_frames", "tile_order", "pixel_spread",
-        "t_helpers", "merged_gather")]
+        "wide_nodes")]
 
 
 class MCPTError(RuntimeError):

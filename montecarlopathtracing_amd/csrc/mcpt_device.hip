@@ -37,22 +37,12 @@
 
 using namespace mcpt;
 
-#ifndef MCPT_PROBE
-#define MCPT_PROBE 0  // sensitivity probes of `make variants` (p1: +1 gather, p2: +16 VALU per node step)
-#endif
 #ifndef MCPT_WAVES_PER_SIMD
 #define MCPT_WAVES_PER_SIMD 4  // k_render occupancy target (tools/sweep.py over `make variants`)
 #endif
 #ifndef MCPT_STACK_WINDOW_K
 #define MCPT_STACK_WINDOW_K 32
 #endif
-#ifndef MCPT_COOP  // cooperative node gathers in k_render's T phase (A/B builds)
-#define MCPT_COOP 0
-#endif
-#ifndef MCPT_COOP_ROUNDS  // their gathers per node step at most (9 nodes each)
-#define MCPT_COOP_ROUNDS 8
-#endif
-constexpr int kLdsPerCu = 160 * 1024;  // gfx950
 constexpr int kStackWindow = MCPT_STACK_WINDOW_K;  // k_render's LDS window when the whole stack would cost occupancy
 
 namespace mcpt {
@@ -186,7 +176,6 @@ constexpr int64_t kPrimSmallTree = 1ll << 20;
 // k_render counters (mcpt_stats): kStatSlots words
 constexpr int kPhaseSlot = 16;     // MCPT_PHASE_TIMING: shader-clock ticks per phase (fetch, T, L, S)
 constexpr int kDebugSlot = 12;     // MCPT_DEBUG: violations of the stack bound, node and triangle indices
-constexpr int kHelpSlot = 20;      // STATS: node steps taken by T-phase helpers
 constexpr int kWaveLogWords = 8;   // MCPT_PHASE_TIMING wave log (mcpt_get_wave_log)
 
 // -DMCPT_DEBUG (make debug -> lib/libmcpt_hip_debug.so): k_render checks every
@@ -379,36 +368,6 @@ struct WindowStack {
   }
   __device__ inline int32_t peek(int sp) const { return lds[((sp - 1) & (K - 1)) * 64]; }  // the top is in the window
 };
-// The same logical stack with its top entry held in a register (k_render,
-// MCPT_TOPREG): entries [0, sp-1) in the inner stack, entry sp-1 in `top`.
-// A pop returns the register at once and refills it from the inner stack,
-// so the LDS read is off the path of the step that uses the popped entry;
-// a peek costs nothing.  A push writes the old top, as the inner push would.
-#ifndef MCPT_TOPREG
-#define MCPT_TOPREG 0
-#endif
-template <class Inner>
-struct TopStack {
-  const Inner &in;
-  int32_t &top;
-  __device__ inline void push(int &sp, int32_t v) const {
-    if (sp > 0) {
-      int t = sp - 1;
-      in.push(t, top);
-    }
-    top = v;
-    ++sp;
-  }
-  __device__ inline int32_t pop(int &sp) const {
-    const int32_t v = top;
-    if (--sp > 0) {
-      int t = sp;
-      top = in.pop(t);
-    }
-    return v;
-  }
-  __device__ inline int32_t peek(int) const { return top; }
-};
 
 // One 4-wide node: slab test of the 4 slots, then pick the slot to enter.
 // NEAREST (the SAH search tree): the passing slot with the smallest entry
@@ -460,82 +419,10 @@ __device__ inline int32_t step4q(f4 q0, f4 q1, f4 q2, f4 q3, f4 q4, f4 q5, int32
   return nxt;
 }
 
-// The value of lane ^ 32 (k_render's T-phase helpers and their partners).
-// MCPT_HELP_XCHG 1: v_permlane32_swap (gfx950; a VALU swap of the wave's
-// halves, no LDS crossbar); 0: ds_bpermute (__shfl_xor).
-#ifndef MCPT_HELP_XCHG
-#define MCPT_HELP_XCHG 0
-#endif
-__device__ inline uint32_t xor32_u(uint32_t v) {
-#if MCPT_HELP_XCHG == 1
-  // vdst lanes 32-63 <- src lanes 0-31, src lanes 0-31 <- vdst lanes 32-63
-  const auto r = __builtin_amdgcn_permlane32_swap(v, v, true, false);
-  return (threadIdx.x & 32u) ? r[0] : r[1];
-#else
-  return (uint32_t)__shfl_xor((int)v, 32);
-#endif
-}
-__device__ inline int32_t xor32_i(int32_t v) { return (int32_t)xor32_u((uint32_t)v); }
-__device__ inline float xor32_f(float v) { return __builtin_bit_cast(float, xor32_u(__builtin_bit_cast(uint32_t, v))); }
-// MCPT_HELP_PAIRING 1: pairs by rank, the k-th offering lane with the k-th
-// free lane (two ds_permute compactions): 28.5 % of C2's node steps helped,
-// against 14.5 % with 0, partners fixed at lane ^ 32 (profiles/r05_helpers_*).
-#ifndef MCPT_HELP_PAIRING
-#define MCPT_HELP_PAIRING 1
-#endif
 // MCPT_POW_LOBE 0: the Phong lobe calls ocml's pow (A/B builds only)
 #ifndef MCPT_POW_LOBE
 #define MCPT_POW_LOBE 1
 #endif
-__device__ inline uint32_t lane_rank(unsigned long long m) {
-  return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-}
-__device__ inline int32_t from_lane(int partner, int32_t v) { return __builtin_amdgcn_ds_bpermute(partner << 2, v); }
-__device__ inline float from_lane_f(int partner, float v) {
-  return __builtin_bit_cast(float, __builtin_amdgcn_ds_bpermute(partner << 2, __builtin_bit_cast(int32_t, v)));
-}
-
-// step4q's choice without its pushes (k_render's T phase with helpers): the
-// slot to enter and the entries to push, in step4q's push order, so the caller
-// can place them on another lane's stack.
-struct Step4Out {
-  int32_t nxt;         // the slot's link, or kPop
-  int32_t p0, p1, p2;  // entries to push (p0 first); at most 3: one passing slot is entered
-  int32_t n;           // how many
-};
-template <bool PRUNE>
-__device__ inline Step4Out select4q(f4 q0, f4 q1, f4 q2, f4 q3, f4 q4, f4 q5, int32_t l0, int32_t l1, int32_t l2,
-                                    int32_t l3, f3 o, f3 rinv, float tmin, float lim, bool nearest) {
-  BoxT b0 = slab_pairs(q0.xy, q0.zw, q1.xy, o, rinv);
-  BoxT b1 = slab_pairs(q1.zw, q2.xy, q2.zw, o, rinv);
-  BoxT b2 = slab_pairs(q3.xy, q3.zw, q4.xy, o, rinv);
-  BoxT b3 = slab_pairs(q4.zw, q5.xy, q5.zw, o, rinv);
-  bool h0 = slab_pass(b0, tmin) && l0 != kEmptySlot, h1 = slab_pass(b1, tmin) && l1 != kEmptySlot;
-  bool h2 = slab_pass(b2, tmin) && l2 != kEmptySlot, h3 = slab_pass(b3, tmin) && l3 != kEmptySlot;
-  if (PRUNE) {
-    h0 = h0 && !(b0.tnear > lim);
-    h1 = h1 && !(b1.tnear > lim);
-    h2 = h2 && !(b2.tnear > lim);
-    h3 = h3 && !(b3.tnear > lim);
-  }
-  const float k0 = nearest ? b0.tnear : 0.0f, k1 = nearest ? b1.tnear : 0.0f;
-  const float k2 = nearest ? b2.tnear : 0.0f, k3 = nearest ? b3.tnear : 0.0f;
-  Step4Out r;
-  r.nxt = kPop;
-  int sel = 4;
-  float kb = __builtin_inff();
-  if (h3) kb = k3, r.nxt = l3, sel = 3;
-  if (h2 && !(k2 > kb)) kb = k2, r.nxt = l2, sel = 2;
-  if (h1 && !(k1 > kb)) kb = k1, r.nxt = l1, sel = 1;
-  if (h0 && !(k0 > kb)) r.nxt = l0, sel = 0;
-  const bool c3 = h3 && sel != 3, c2 = h2 && sel != 2, c1 = h1 && sel != 1, c0 = h0 && sel != 0;
-  r.p0 = c3 ? l3 : (c2 ? l2 : (c1 ? l1 : l0));
-  r.p1 = c3 ? (c2 ? l2 : (c1 ? l1 : l0)) : (c2 ? (c1 ? l1 : l0) : l0);
-  r.p2 = l0;  // a third push is only ever l0 (c3, c2 and c1 among the first two, or l1 after two of them)
-  r.n = (int32_t)c3 + (int32_t)c2 + (int32_t)c1 + (int32_t)c0;
-  if (r.n == 3 && !c0) r.p2 = l1;  // c3 c2 c1: the third is l1
-  return r;
-}
 
 // Result rule of the EXACT search.  The reference keeps the
 // first triangle in its DFS order and replaces it only by one at least EPS
@@ -937,8 +824,6 @@ struct RenderArgs {
   const int32_t *tile_order;  // queue position -> 8x8 tile (dearest first, mcpt_tuning.tile_order), or nullptr: image order
   uint32_t *entry_log;        // MCPT_PHASE_TIMING: per (pixel, block) claim / start / end times (mcpt_get_entry_log), or nullptr
   int32_t spread;             // 1: each run of 64 queue slots takes one pixel from each of 64 tiles (mcpt_tuning.pixel_spread)
-  int32_t coop_off;           // COOP: byte offset of the node staging in LDS
-  int32_t coop_nmax;          // COOP: nodes the staging holds
 };
 
 __device__ inline int32_t global_row(int32_t lr, const RenderArgs &A) {
@@ -977,16 +862,11 @@ __device__ inline uint32_t queue_items(uint32_t x, uint32_t n_tiles, uint32_t nq
 // PRIM: the primary-hit pass (PrimHit) run by the same machine: one frame,
 // no pixel state; a lane traces its pixel's primary ray, stores the closest
 // hit at the S phase instead of shading, and takes the next pixel.
-// VAR: 0 the plain phases, 1 T-phase helpers (t_helpers), 2 merged T / L
-// gathers (merged_gather)
-template <int MODE, bool STATS, bool WIN, bool PAIR, bool Q, bool PRIM = false, bool G = true, int VAR = 0>
+template <int MODE, bool STATS, bool WIN, bool PAIR, bool Q, bool PRIM = false, bool G = true>
 __global__ void __launch_bounds__(64, MCPT_WAVES_PER_SIMD) k_render(RenderArgs A) {
   constexpr bool PRUNE = MODE != MCPT_MODE_NOPRUNE;
   constexpr bool LIT = MODE == MCPT_MODE_NOPRUNE;
-  constexpr bool HELP = VAR == 1, MERGE = VAR == 2;
   static_assert(!(Q && LIT), "the quantized search tree is an EXACT-mode structure");
-  static_assert(!(HELP && (LIT || PRIM)), "T-phase helpers serve the EXACT search only");
-  static_assert(!(MERGE && (LIT || PRIM || Q)), "merged gathers: the EXACT search over 128-B nodes");
   extern __shared__ int32_t lds_stack[];
   const int lane = threadIdx.x;
   // the whole stack in LDS, or its top kStackWindow entries (deep trees, where
@@ -1025,7 +905,7 @@ __global__ void __launch_bounds__(64, MCPT_WAVES_PER_SIMD) k_render(RenderArgs A
 
   unsigned long long n_seg = 0, n_nodes = 0, n_tests = 0, n_bad = 0;
   unsigned long long w_t = 0, w_l = 0, w_s = 0, n_fb = 0;
-  unsigned long long w_it = 0, n_wait = 0, n_idle = 0, n_rej = 0, n_help = 0;
+  unsigned long long w_it = 0, n_wait = 0, n_idle = 0, n_rej = 0;
   uint32_t px_seg = 0, px_it = 0;  // STATS: segments / busy iterations of the lane's current entry (A.px_*)
   // pixel state.  lst: this lane's role in the queue protocol, one small
   // int (one VGPR; kept out of lane-mask SGPR pairs on purpose, SGPRs are
@@ -1054,17 +934,7 @@ __global__ void __launch_bounds__(64, MCPT_WAVES_PER_SIMD) k_render(RenderArgs A
   // traverse_exact); t2 = runner-up t of the nearest-first search
   bool ref = LIT;
   float t2 = kFltMax;
-  // the stack the phases use: the LDS stack, or (TOPREG, plain phases only)
-  // the same stack with its top in a register
-  constexpr bool TOPREG = MCPT_TOPREG && VAR == 0;
-  constexpr bool COOP = MCPT_COOP && VAR == 0 && !LIT && !Q && !PRIM;
-  int32_t tos = 0;
-  const auto sk = [&] {
-    if constexpr (TOPREG)
-      return TopStack<Stack>{stk, tos};
-    else
-      return stk;
-  }();
+  const Stack &sk = stk;
   auto pop_next = [&]() -> int32_t { return sp == 0 ? kDone : sk.pop(sp); };
   auto begin_segment = [&]() {
     rinv.x = __builtin_amdgcn_rcpf(d.x);
@@ -1268,7 +1138,7 @@ __global__ void __launch_bounds__(64, MCPT_WAVES_PER_SIMD) k_render(RenderArgs A
       n_idle += lst == kNeed || lst == kDead;  // no claim yet, an edge hole, or out of work (tail)
     }
     // one triangle test with the reference's arithmetic and result rule (the
-    // L phase, and the merged gathers' leaf lanes)
+    // L phase)
     using Tri = typename std::conditional<Q, DevTriQ, DevTri>::type;
     auto test = [&](const Tri &X, int32_t xi) {
       TriHit h;
@@ -1313,244 +1183,8 @@ __global__ void __launch_bounds__(64, MCPT_WAVES_PER_SIMD) k_render(RenderArgs A
     };
     // ---- T: one node step (objdef.h:252-273 with child boxes)
     const bool in_t = live && cur >= 0;
-    if constexpr (HELP) {
-      // T-phase helpers: a lane not stepping this iteration
-      // (waiting for L or S, or out of work) steps its partner lane's (lane ^
-      // 32) stack-top node in the same instructions, and pushes what it finds
-      // onto the partner's stack: one gather serves two nodes of one ray, so
-      // the ray's search takes fewer iterations.  EXACT's answer depends only
-      // on the candidate set (pruning with the partner's bound at the time is
-      // safe: it only prunes less than later) and on the order-free t1 / t2
-      // rule; the reference-order search (ref) is never helped.
-      const unsigned long long mt = __ballot(in_t);
-      if (mt) {
-        if (STATS && lane == __builtin_ctzll(__ballot(1))) w_t++;
-        // offer the stack's top when it is an internal node and the stack has
-        // room for both steps' pushes (the owner's 3, the helper's 3 + 1)
-        int32_t top = -1;
-        if (in_t && !ref && sp > 0 && sp + 6 <= stack_cap) top = sk.peek(sp);
-        const unsigned long long mw = __ballot(top >= 0);
-#if MCPT_HELP_PAIRING == 1
-        // the k-th offering lane with the k-th free lane: every lane sends its
-        // id to its rank's slot (a permutation: others after the listed ones),
-        // then reads its partner's id from the other list
-        const unsigned long long mf = ~mt;
-        const int n_w = __popcll(mw), n_f = __popcll(mf), n_pair = min(n_w, n_f);
-        const bool is_w = top >= 0, is_f = !in_t;
-        const uint32_t r_w = lane_rank(is_w ? mw : ~mw), r_f = lane_rank(is_f ? mf : ~mf);
-        const int32_t wlist = __builtin_amdgcn_ds_permute((int)((is_w ? r_w : n_w + r_w) << 2), lane);
-        const int32_t flist = __builtin_amdgcn_ds_permute((int)((is_f ? r_f : n_f + r_f) << 2), lane);
-        const bool give = is_w && (int)r_w < n_pair;
-        const bool help = is_f && (int)r_f < n_pair;
-        const int32_t h_of_w = from_lane((int)r_w & 63, flist), w_of_f = from_lane((int)r_f & 63, wlist);
-        const int partner = give ? h_of_w : (help ? w_of_f : lane);
-        auto xchg_i = [&](int32_t v) { return from_lane(partner, v); };
-        auto xchg_f = [&](float v) { return from_lane_f(partner, v); };
-#else
-        const int partner = lane ^ 32;
-        const bool give = top >= 0 && !((mt >> partner) & 1ull);
-        const bool help = !in_t && ((mw >> partner) & 1ull);
-        auto xchg_i = [&](int32_t v) { return xor32_i(v); };
-        auto xchg_f = [&](float v) { return xor32_f(v); };
-#endif
-        if (give) (void)sk.pop(sp);
-        const float lim_own = best_t + S.prune_margin;
-        int32_t wn = cur;
-        f3 wo = o.xyz, wr = rinv;
-        float wlim = lim_own;
-        if (__ballot(help)) {  // what a helper borrows: the entry, the ray, the pruning bound
-          const int32_t g_n = xchg_i(top);
-          const f3 g_o = (f3){xchg_f(o.x), xchg_f(o.y), xchg_f(o.z)};
-          const f3 g_r = (f3){xchg_f(rinv.x), xchg_f(rinv.y), xchg_f(rinv.z)};
-          const float g_lim = xchg_f(lim_own);
-          if (help) wn = g_n, wo = g_o, wr = g_r, wlim = g_lim;
-        }
-        const bool act = in_t || help;
-        const bool wref = ref && !help;
-        Step4Out so;
-        so.nxt = kPop, so.p0 = so.p1 = so.p2 = 0, so.n = 0;
-        if (act && MCPT_DCHECK(wn < (wref ? S.n_nodes4 : S.n_near4), 1)) {
-          f4 q0, q1, q2, q3, q4, q5;
-          int32_t l0, l1, l2, l3;
-          if (Q && !wref) {
-            const f4 *p = reinterpret_cast<const f4 *>(S.near4q + wn);
-            const f4 c0 = p[0], c1 = p[1], c2 = p[2], c3 = p[3];
-            const float ox = c0.x, oy = c0.y, oz = c0.z, sx = c0.w, sy = c2.z, sz = c2.w;
-            auto dec = [](uint32_t w, float sa, float oa, float sb, float ob) -> f4 {
-              return (f4){__builtin_fmaf((float)(w & 0xFFu), sa, oa), __builtin_fmaf((float)((w >> 8) & 0xFFu), sa, oa),
-                          __builtin_fmaf((float)((w >> 16) & 0xFFu), sb, ob), __builtin_fmaf((float)(w >> 24), sb, ob)};
-            };
-            q0 = dec(as_u(c1.x), sx, ox, sy, oy);
-            q1 = dec(as_u(c1.y), sz, oz, sx, ox);
-            q2 = dec(as_u(c1.z), sy, oy, sz, oz);
-            q3 = dec(as_u(c1.w), sx, ox, sy, oy);
-            q4 = dec(as_u(c2.x), sz, oz, sx, ox);
-            q5 = dec(as_u(c2.y), sy, oy, sz, oz);
-            l0 = as_i(c3.x), l1 = as_i(c3.y), l2 = as_i(c3.z), l3 = as_i(c3.w);
-          } else {
-            const DevNode4 &N = (wref ? S.nodes4 : S.near4)[wn];
-            q0 = N.q[0], q1 = N.q[1], q2 = N.q[2], q3 = N.q[3], q4 = N.q[4], q5 = N.q[5];
-            l0 = N.link[0], l1 = N.link[1], l2 = N.link[2], l3 = N.link[3];
-          }
-          so = select4q<PRUNE>(q0, q1, q2, q3, q4, q5, l0, l1, l2, l3, wo, wr, kTmin, wlim, !wref);
-          if (STATS) n_nodes++, n_help += help;
-        }
-        // a T lane whose pushes would overflow the stack (helpers' entries can
-        // grow it beyond the single search's bound) restarts the segment as the
-        // reference-order search, from an empty stack: the exact fallback
-        const bool ovf = in_t && !ref && sp + so.n > stack_cap;
-        const int32_t own_end = sp + (in_t && !ovf ? so.n : 0);
-        const int32_t p_end = xchg_i(own_end);
-        // pushes: a T lane's onto its own stack, a helper's onto its partner's,
-        // above the partner's own, then the helper's chosen child on top
-        const int32_t np = ovf || !act ? 0 : so.n + (help && so.nxt != kPop ? 1 : 0);
-        const int col = help ? partner : lane;
-        const int32_t base = help ? p_end : sp;
-        for (int k = 0; k < 4; ++k) {
-          if (k < np) {
-            const int32_t v = k == 0 ? (so.n > 0 ? so.p0 : so.nxt)
-                                     : (k == 1 ? (so.n > 1 ? so.p1 : so.nxt) : (k == 2 ? (so.n > 2 ? so.p2 : so.nxt) : so.nxt));
-            const int32_t idx = base + k;
-            if constexpr (WIN) {
-              int32_t *slot = lds_stack + col + (idx & (kStackWindow - 1)) * 64;
-              if (idx >= kStackWindow)
-                A.spill[((size_t)blockIdx.x * 64 + col) * (size_t)A.spill_stride + (idx - kStackWindow)] = *slot;
-              *slot = v;
-            } else {
-              lds_stack[col + idx * 64] = v;
-            }
-          }
-        }
-        const int32_t h_add = xchg_i(help ? np : 0);
-        if (in_t) {
-          if (ovf) {
-            if (STATS) n_fb++;
-            ref = true;
-            best_t = kFltMax;
-            t2 = kFltMax;
-            sp = 0;
-            cur = S.root_leaf >= 0 ? ~S.root_leaf : 0;  // the root box passed: the segment was being searched
-          } else {
-            sp = own_end + (give ? h_add : 0);
-            if (!MCPT_DCHECK(sp <= stack_cap, 0)) sp = stack_cap;
-            cur = so.nxt;
-            if (cur == kPop) cur = pop_next();
-          }
-        }
-      }
-    } else if constexpr (MERGE) {
-      // Merged gathers: the lanes holding a leaf at the
-      // iteration's start whose L phase runs now (the same threshold rule)
-      // fetch their triangles in the T phase's load instructions -- each
-      // gather takes a node for a T lane and a triangle (or the paired two)
-      // for an L lane -- so an iteration that runs both phases waits for one
-      // gather, and the L phase's own gather instructions disappear.  A lane
-      // whose T step ends on a leaf tests it next iteration; its sequence of
-      // operations is unchanged, and so are the bits.
-      const unsigned long long mt = __ballot(in_t);
-      const bool in_l0 = live && cur < 0 && cur != kDone;
-      const unsigned long long ml0 = __ballot(in_l0);
-      const bool run_l = ml0 && (__popcll(ml0) >= th_leaf || !mt);
-      if (mt || run_l) {
-        if (STATS && lane == __builtin_ctzll(__ballot(1))) {
-          if (mt) w_t++;
-          if (run_l) w_l++;
-        }
-        const bool gl = run_l && in_l0;
-        const int32_t nx = (PAIR && gl && sp > 0) ? sk.peek(sp) : kDone;
-        const bool two = PAIR && gl && nx < 0 && nx != kDone;
-        const int32_t ti = gl && MCPT_DCHECK(~cur < S.n_tris, 2) ? ~cur : 0;
-        const int32_t ti2 = two && MCPT_DCHECK(~nx < S.n_tris, 2) ? ~nx : 0;
-        const DevNode4 *__restrict__ tree = ref ? S.nodes4 : S.near4;
-        const bool node_ok = in_t && MCPT_DCHECK(cur < (ref ? S.n_nodes4 : S.n_near4), 1);
-        const f4 *a = in_t ? reinterpret_cast<const f4 *>(tree + (node_ok ? cur : 0))
-                           : reinterpret_cast<const f4 *>(S.tris + ti);
-        const f4 *b = in_t ? a + 3 : reinterpret_cast<const f4 *>(S.tris + ti2);
-        f4 g0 = (f4){0.0f, 0.0f, 0.0f, 0.0f}, g1 = g0, g2 = g0, g3 = g0, g4 = g0, g5 = g0, g6 = g0;
-        if (in_t || gl) g0 = a[0], g1 = a[1], g2 = a[2];  // node planes 0-2, or the triangle's 48 B
-        if (in_t || two) g3 = b[0], g4 = b[1], g5 = b[2];  // node planes 3-5, or the paired triangle
-        if (in_t) g6 = a[6];                              // node links
-        if (in_t) {
-          uint32_t ctr = 0;
-          if (node_ok) {
-            cur = step4q<PRUNE>(g0, g1, g2, g3, g4, g5, as_i(g6.x), as_i(g6.y), as_i(g6.z), as_i(g6.w), o.xyz, rinv,
-                                kTmin, best_t + S.prune_margin, !ref, sk, sp, ctr);
-            if (!MCPT_DCHECK(sp <= stack_cap, 0)) sp = stack_cap;
-          } else {
-            cur = kPop;
-          }
-          if (STATS) n_nodes += ctr;
-          if (cur == kPop) cur = pop_next();
-        }
-        if (gl) {
-          Tri X{};
-          X.v0 = g0, X.nab = g1, X.nac = g2;
-          test(X, ti);
-          if (two) {
-            (void)sk.pop(sp);
-            X.v0 = g3, X.nab = g4, X.nac = g5;
-            test(X, ti2);
-          }
-          cur = pop_next();
-        }
-      }
-    } else if (__ballot(in_t)) {
+    if (__ballot(in_t)) {
       if (STATS && lane == __builtin_ctzll(__ballot(1))) w_t++;
-      // COOP (cooperative node gathers): the wave fetches its T lanes' nodes
-      // seven lanes to a node, one 16-B chunk each, nine nodes per
-      // instruction, into an LDS staging area (MCPT_COOP 1: global_load_lds;
-      // 2: into registers, then ds_write); each T lane then reads its node
-      // from LDS.  An instruction touches 9 lines instead of one per T lane,
-      // and a node step issues ceil(T lanes / 9) gathers instead of 7.  T
-      // lanes ranked past the staging area (A.coop_nmax nodes) gather their
-      // own node as before.  Same nodes, same bits.
-      bool staged = false;
-      const f4 *cgp = nullptr;  // COOP: this lane's staged node in LDS
-      if constexpr (COOP) {
-        const unsigned long long mt = __ballot(in_t);
-        const int nt = __popcll(mt);
-        const int nst = nt < A.coop_nmax ? nt : A.coop_nmax;
-        const bool node_ok = in_t && MCPT_DCHECK(cur < (ref ? S.n_nodes4 : S.n_near4), 1);
-        const uint32_t rk_t = lane_rank(mt);
-        // a permutation of the lanes: T lanes to their rank, the others after them
-        const uint32_t rk = in_t ? rk_t : (uint32_t)nt + lane_rank(~mt);
-        const int32_t gid = node_ok ? (ref ? S.n_near4 + cur : cur) : -1;
-        const int32_t byrank = __builtin_amdgcn_ds_permute((int)(rk << 2), gid);  // lane j: rank j's node
-        const int grp = lane / 7, ch = lane - 7 * grp;
-        char *const stage = reinterpret_cast<char *>(lds_stack) + A.coop_off;
-        constexpr int R = MCPT_COOP_ROUNDS;  // rounds: up to 9 R nodes staged (A.coop_nmax <= 9 R)
-        int32_t gk[R];
-#pragma unroll
-        for (int k = 0; k < R; ++k)  // every round's node id first: one LDS wait, not one per round
-          gk[k] = 9 * k < nst ? __builtin_amdgcn_ds_bpermute(((9 * k + grp) & 63) << 2, byrank) : -1;
-        auto chunk = [&](int k) -> const f4 * {
-          const int32_t g = gk[k];
-          const DevNode4 *nb = g < S.n_near4 ? S.near4 + g : S.nodes4 + (g - S.n_near4);
-          return reinterpret_cast<const f4 *>(nb) + ch;
-        };
-        if constexpr (MCPT_COOP == 1) {
-          typedef __attribute__((address_space(3))) void LdsVoid;
-#pragma unroll
-          for (int k = 0; k < R; ++k)
-            if (9 * k < nst && grp < 9 && 9 * k + grp < nst && gk[k] >= 0)
-              __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void *)chunk(k),
-                                               (LdsVoid *)(stage + k * 9 * 112), 16, 0, 0);
-          __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): the staged nodes are in LDS (hipcc does not count LDS-DMA)
-          __asm__ __volatile__("" ::: "memory");
-        } else {
-          typedef __attribute__((address_space(3))) f4 LdsF4w;
-          f4 v[R];
-#pragma unroll
-          for (int k = 0; k < R; ++k)
-            if (9 * k < nst && grp < 9 && 9 * k + grp < nst && gk[k] >= 0) v[k] = *chunk(k);
-#pragma unroll
-          for (int k = 0; k < R; ++k)
-            if (9 * k < nst && grp < 9 && 9 * k + grp < nst && gk[k] >= 0)
-              *(LdsF4w *)(stage + k * 9 * 112 + lane * 16) = v[k];
-        }
-        staged = in_t && (int)rk_t < nst && node_ok;
-        cgp = reinterpret_cast<const f4 *>(stage + rk_t * 112);
-      }
       if (in_t) {
         if (Q) {  // EXACT, quantized SAH tree nearest-first (4 loads), or the reference tree left-first
           uint32_t ctr = 0;
@@ -1589,38 +1223,7 @@ __global__ void __launch_bounds__(64, MCPT_WAVES_PER_SIMD) k_render(RenderArgs A
           uint32_t ctr = 0;
           const DevNode4 *__restrict__ tree = ref ? S.nodes4 : S.near4;
           if (MCPT_DCHECK(cur < (ref ? S.n_nodes4 : S.n_near4), 1)) {
-#if MCPT_PROBE == 1  // sensitivity probe (not shipped): one more 16-B gather per node step
-            const f4 pad = tree[cur].pad;
-#elif MCPT_PROBE == 3  // one more 4-B gather per node step (same line)
-            const f4 pad = (f4){reinterpret_cast<const float *>(&tree[cur].pad)[0], 0.0f, 0.0f, 0.0f};
-#elif MCPT_PROBE == 4  // one more 16-B load per node step, the same address in every lane
-            const f4 pad = tree[0].pad;
-#endif
-            if constexpr (COOP) {  // the staged node (LDS-typed reads: ds_read_b128), or an overflow lane's own
-              typedef const __attribute__((address_space(3))) f4 LdsF4;
-              f4 c0, c1, c2, c3, c4, c5, c6;
-              if (staged) {
-                LdsF4 *q = (LdsF4 *)cgp;
-                c0 = q[0], c1 = q[1], c2 = q[2], c3 = q[3], c4 = q[4], c5 = q[5], c6 = q[6];
-              } else {
-                const f4 *q = reinterpret_cast<const f4 *>(tree + cur);
-                c0 = q[0], c1 = q[1], c2 = q[2], c3 = q[3], c4 = q[4], c5 = q[5], c6 = q[6];
-              }
-              cur = step4q<PRUNE>(c0, c1, c2, c3, c4, c5, as_i(c6.x), as_i(c6.y), as_i(c6.z), as_i(c6.w), o.xyz, rinv,
-                                  kTmin, best_t + S.prune_margin, !ref, sk, sp, ctr);
-            } else {
-              cur = step4<PRUNE>(tree[cur], o.xyz, rinv, kTmin, best_t + S.prune_margin, !ref, sk, sp, ctr);
-            }
-#if MCPT_PROBE == 1 || MCPT_PROBE == 3 || MCPT_PROBE == 4
-            if (__builtin_expect(as_i(pad.x) == 0x7FC0DEAD, 0)) cur = kPop;
-#elif MCPT_PROBE == 2  // sensitivity probe (not shipped): 16 more VALU per node step
-            {
-              float x = rinv.x;
-#pragma unroll
-              for (int k = 0; k < 16; ++k) x = fmaf(x, 1.0001f, rinv.y);
-              if (__builtin_expect(as_i(x) == 0x7FC0DEAD, 0)) cur = kPop;
-            }
-#endif
+            cur = step4<PRUNE>(tree[cur], o.xyz, rinv, kTmin, best_t + S.prune_margin, !ref, sk, sp, ctr);
             if (!MCPT_DCHECK(sp <= stack_cap, 0)) sp = stack_cap;
           } else {
             cur = kPop;
@@ -1645,10 +1248,10 @@ __global__ void __launch_bounds__(64, MCPT_WAVES_PER_SIMD) k_render(RenderArgs A
       }
     }
     MCPT_TICK(1);
-    // ---- L: triangle tests, batched (MERGE: run with the T phase's gathers)
-    const bool in_l = !MERGE && live && cur < 0 && cur != kDone;
+    // ---- L: triangle tests, batched
+    const bool in_l = live && cur < 0 && cur != kDone;
     const unsigned long long ml = __ballot(in_l);
-    if (!MERGE && ml && (__popcll(ml) >= th_leaf || !__ballot(live && cur >= 0))) {
+    if (ml && (__popcll(ml) >= th_leaf || !__ballot(live && cur >= 0))) {
       if (STATS && lane == __builtin_ctzll(__ballot(1))) w_l++;
       if (in_l) {
         // PAIR (MCPT_SCHED_PAIRED): when the next stack entry is a leaf too,
@@ -1824,7 +1427,6 @@ __global__ void __launch_bounds__(64, MCPT_WAVES_PER_SIMD) k_render(RenderArgs A
     if (n_wait) atomicAdd(&A.stats[9], n_wait);
     if (n_idle) atomicAdd(&A.stats[10], n_idle);
     if (n_rej) atomicAdd(&A.stats[11], n_rej);
-    if (n_help) atomicAdd(&A.stats[kHelpSlot], n_help);
   }
 }
 
@@ -2074,17 +1676,29 @@ __global__ void k_selfcheck_trig(uint32_t n, int angles, unsigned long long *bad
   if (!ok) atomicAdd(bad, 1ull);
 }
 
+// The self-checks count mismatches in a scratch allocation of their own (not
+// ctx->d_stats, which holds the last stats render's counters until
+// mcpt_get_stats reads them), freed on every exit path.
+struct DevScratch {
+  void *p = nullptr;
+  ~DevScratch() {
+    if (p) (void)hipFree(p);
+  }
+};
+
 int mcpt_selfcheck_trig(mcpt_ctx *c, int64_t *angle_bad, int64_t *range_bad) {
   if (!c || !angle_bad || !range_bad) return mcpt::fail(MCPT_ERR_ARG, "selfcheck_trig: null");
   HIP_OK(hipSetDevice(c->device));
-  HIP_OK(hipMemset(c->d_stats, 0, 2 * sizeof(unsigned long long)));
+  DevScratch scr;
+  HIP_OK(hipMalloc(&scr.p, 2 * sizeof(unsigned long long)));
+  unsigned long long *bad = (unsigned long long *)scr.p;
+  HIP_OK(hipMemset(bad, 0, 2 * sizeof(unsigned long long)));
   const uint32_t n_range = 0x41000000u;  // bit patterns of [0, 8.0f)
-  hipLaunchKernelGGL(k_selfcheck_trig, dim3(32768 / 256), dim3(256), 0, 0, 32768u, 1, c->d_stats);
-  hipLaunchKernelGGL(k_selfcheck_trig, dim3((n_range + 255) / 256), dim3(256), 0, 0, n_range, 0,
-                     c->d_stats + 1);
+  hipLaunchKernelGGL(k_selfcheck_trig, dim3(32768 / 256), dim3(256), 0, 0, 32768u, 1, bad);
+  hipLaunchKernelGGL(k_selfcheck_trig, dim3((n_range + 255) / 256), dim3(256), 0, 0, n_range, 0, bad + 1);
   HIP_OK(hipGetLastError());
   unsigned long long h[2];
-  HIP_OK(hipMemcpy(h, c->d_stats, sizeof(h), hipMemcpyDeviceToHost));
+  HIP_OK(hipMemcpy(h, bad, sizeof(h), hipMemcpyDeviceToHost));
   *angle_bad = (int64_t)h[0];
   *range_bad = (int64_t)h[1];
   return MCPT_OK;
@@ -2108,15 +1722,16 @@ __global__ void __launch_bounds__(256) k_selfcheck_pow(const float *ys, int32_t 
 int mcpt_selfcheck_pow(mcpt_ctx *c, const float *ys, int32_t n, int64_t *mismatches) {
   if (!c || !ys || n <= 0 || n > 4096 || !mismatches) return mcpt::fail(MCPT_ERR_ARG, "selfcheck_pow: bad argument");
   HIP_OK(hipSetDevice(c->device));
-  float *dy = nullptr;
-  HIP_OK(hipMalloc(&dy, (size_t)n * sizeof(float)));
+  DevScratch scr;  // the counter, then the exponents
+  HIP_OK(hipMalloc(&scr.p, 16 + (size_t)n * sizeof(float)));
+  unsigned long long *bad = (unsigned long long *)scr.p;
+  float *dy = (float *)((char *)scr.p + 16);
   HIP_OK(hipMemcpy(dy, ys, (size_t)n * sizeof(float), hipMemcpyHostToDevice));
-  HIP_OK(hipMemset(c->d_stats, 0, sizeof(unsigned long long)));
-  hipLaunchKernelGGL(k_selfcheck_pow, dim3((unsigned)(c->n_cu * 16)), dim3(256), 0, 0, dy, n, c->d_stats);
+  HIP_OK(hipMemset(bad, 0, sizeof(unsigned long long)));
+  hipLaunchKernelGGL(k_selfcheck_pow, dim3((unsigned)(c->n_cu * 16)), dim3(256), 0, 0, dy, n, bad);
   HIP_OK(hipGetLastError());
   unsigned long long h = 0;
-  HIP_OK(hipMemcpy(&h, c->d_stats, sizeof(h), hipMemcpyDeviceToHost));
-  (void)hipFree(dy);
+  HIP_OK(hipMemcpy(&h, bad, sizeof(h), hipMemcpyDeviceToHost));
   *mismatches = (int64_t)h;
   return MCPT_OK;
 }
@@ -2272,7 +1887,6 @@ int mcpt_get_stats(mcpt_ctx *c, mcpt_stats *out) {
       c->last.lane_waiting = h[9];
       c->last.lane_idle = h[10];
       c->last.leaf_rejects = h[11];
-      c->last.helped_steps = h[kHelpSlot];
       c->last.debug_violations = h[kDebugSlot] + h[kDebugSlot + 1] + h[kDebugSlot + 2];
       for (int k = 0; k < 4; ++k) c->last.phase_ticks[k] = h[kPhaseSlot + k];
     }
@@ -2310,8 +1924,7 @@ int mcpt_set_tuning(mcpt_ctx *c, const mcpt_tuning *t) {
             t->primary_cache < 0 || t->primary_cache > 2 || t->lds_pad < 0 || t->lds_pad > 65536 ||
             t->queue_chunk > 4096 || t->leaf_threshold > 64 || t->shade_threshold > 64 || t->fetch_threshold > 64 ||
             t->last_block_frames < -1 || t->tile_order < 0 || t->tile_order > 2 || t->pixel_spread < 0 ||
-            t->pixel_spread > 2 || t->t_helpers < 0 || t->t_helpers > 2 || t->merged_gather < 0 ||
-            t->merged_gather > 2))
+            t->pixel_spread > 2))
     return mcpt::fail(MCPT_ERR_ARG, "set_tuning: value out of range");
   if (t)
     c->tune = *t;
@@ -2816,18 +2429,14 @@ int mcpt_render_frames(mcpt_ctx *ctx, const mcpt_scene *scene, const mcpt_camera
   // The stack lives in LDS; when the whole stack would allow fewer resident
   // workgroups than a kStackWindow window does, the windowed kernel runs.
   const bool noprune = p->mode == MCPT_MODE_NOPRUNE;
-  // [kind: 0 EXACT 128-B nodes, 1 NOPRUNE, 2 EXACT quantized][stats][window][pair]
-  // [glossy materials][variant: plain, T-phase helpers (EXACT), merged gathers
-  // (EXACT, 128-B nodes); a slot a kind does not have holds its plain kernel]
-#define MCPT_KH(M, ST, W, P, QN, GL) {(const void *)k_render<M, ST, W, P, QN, false, GL, 0>, \
-                                      (const void *)k_render<M, ST, W, P, QN, false, GL, (M != MCPT_MODE_NOPRUNE) ? 1 : 0>, \
-                                      (const void *)k_render<M, ST, W, P, QN, false, GL, (M != MCPT_MODE_NOPRUNE && !QN) ? 2 : 0>}
-#define MCPT_KG(M, ST, W, P, QN) {MCPT_KH(M, ST, W, P, QN, false), MCPT_KH(M, ST, W, P, QN, true)}
+  // [kind: 0 EXACT 128-B nodes, 1 NOPRUNE, 2 EXACT quantized][stats][window][pair][glossy materials]
+#define MCPT_KG(M, ST, W, P, QN) {(const void *)k_render<M, ST, W, P, QN, false, false>, \
+                                  (const void *)k_render<M, ST, W, P, QN, false, true>}
 #define MCPT_KR(M, ST, W, QN) {MCPT_KG(M, ST, W, false, QN), MCPT_KG(M, ST, W, true, QN)}
 #define MCPT_KK(M, QN) {{MCPT_KR(M, false, false, QN), MCPT_KR(M, false, true, QN)}, \
                         {MCPT_KR(M, true, false, QN), MCPT_KR(M, true, true, QN)}}
-  static const void *const kfns[3][2][2][2][2][3] = {MCPT_KK(MCPT_MODE_EXACT, false), MCPT_KK(MCPT_MODE_NOPRUNE, false),
-                                                     MCPT_KK(MCPT_MODE_EXACT, true)};
+  static const void *const kfns[3][2][2][2][2] = {MCPT_KK(MCPT_MODE_EXACT, false), MCPT_KK(MCPT_MODE_NOPRUNE, false),
+                                                  MCPT_KK(MCPT_MODE_EXACT, true)};
   // the primary-hit pass: [kind][window][pair], no stats
 #define MCPT_KP(M, W, QN) {(const void *)k_render<M, false, W, false, QN, true, false>, \
                            (const void *)k_render<M, false, W, true, QN, true, false>}
@@ -2838,7 +2447,6 @@ int mcpt_render_frames(mcpt_ctx *ctx, const mcpt_scene *scene, const mcpt_camera
 #undef MCPT_KK
 #undef MCPT_KR
 #undef MCPT_KG
-#undef MCPT_KH
   // quantized search tree: forced on (1) or off (2), or auto (0): on when the
   // 128-B tree outgrows the GPU's aggregate L2, where its halved node bytes and
   // gathers pay (C5 -6 %); on cache-resident trees its looser boxes cost more
@@ -2847,50 +2455,31 @@ int mcpt_render_frames(mcpt_ctx *ctx, const mcpt_scene *scene, const mcpt_camera
   const bool quant = scene->near4q && (T.quantized == 1 || (T.quantized == 0 && scene->near4_bytes > kQuantAutoBytes));
   const int kind = noprune ? 1 : (quant ? 2 : 0);
   const int glossy = scene->has_glossy ? 1 : 0;  // the shading instantiation (speed only: same bits)
-  // the kernel's variant: T-phase helpers (EXACT; t_helpers 2) or merged
-  // T / L gathers (EXACT over the 128-B nodes; merged_gather 2); auto (0): plain
-  const int help = !noprune && T.t_helpers == 2 ? 1 : (!noprune && !quant && T.merged_gather == 2 ? 2 : 0);
   const size_t pad = (size_t)std::max(0, T.lds_pad);
-  // COOP builds (MCPT_COOP): the cooperative node gathers' LDS staging follows
-  // the uniforms and the material table, as many 112-B nodes as the LDS
-  // leaves per wave at the kernel's occupancy target (at least one gather's 9)
-  const bool coop = MCPT_COOP && kind == 0 && help == 0;
-  const size_t base_plain = ((size_t)depth_entries * 64 * sizeof(int32_t) + sizeof(LdsUniforms) + lds_mats + 15) & ~(size_t)15;
-  const size_t base_win = ((size_t)kStackWindow * 64 * sizeof(int32_t) + sizeof(LdsUniforms) + lds_mats + 15) & ~(size_t)15;
-  auto coop_nodes = [&](size_t base) -> int {
-    if (!coop) return 0;
-    const size_t budget = (size_t)kLdsPerCu / (4 * MCPT_WAVES_PER_SIMD);
-    if (base + pad + 9 * 112 > budget) return 9;
-    return (int)std::min<size_t>(std::min(64, 9 * MCPT_COOP_ROUNDS), (budget - base - pad) / 112);
-  };
-  const int coop_plain = coop_nodes(base_plain), coop_win = coop_nodes(base_win);
-  const size_t lds_plain = base_plain + (size_t)coop_plain * 112 + pad;
-  const size_t lds_win = base_win + (size_t)coop_win * 112 + pad;
+  const size_t lds_plain = (((size_t)depth_entries * 64 * sizeof(int32_t) + sizeof(LdsUniforms) + lds_mats + 15) & ~(size_t)15) + pad;
+  const size_t lds_win = (((size_t)kStackWindow * 64 * sizeof(int32_t) + sizeof(LdsUniforms) + lds_mats + 15) & ~(size_t)15) + pad;
   bool win = false;
   int per_cu = 0;
   if (T.stack_window == 1) {  // forced (tests, experiments): the window even when the whole stack fits in it
     win = true;
-    rc = occupancy(ctx, kfns[kind][ctx->stats_on][1][pair][glossy][help], lds_win, &per_cu);
+    rc = occupancy(ctx, kfns[kind][ctx->stats_on][1][pair][glossy], lds_win, &per_cu);
     if (rc) return rc;
   } else if (depth_entries > kStackWindow && T.stack_window != 2) {
     int per_cu_plain = 0, per_cu_win = 0;
-    rc = occupancy(ctx, kfns[kind][ctx->stats_on][0][pair][glossy][help], lds_plain, &per_cu_plain);
+    rc = occupancy(ctx, kfns[kind][ctx->stats_on][0][pair][glossy], lds_plain, &per_cu_plain);
     if (rc) return rc;
-    rc = occupancy(ctx, kfns[kind][ctx->stats_on][1][pair][glossy][help], lds_win, &per_cu_win);
+    rc = occupancy(ctx, kfns[kind][ctx->stats_on][1][pair][glossy], lds_win, &per_cu_win);
     if (rc) return rc;
-    // COOP: at equal occupancy the window, whose smaller stack leaves more staging
-    win = T.stack_window == 1 || per_cu_win > per_cu_plain || (coop && per_cu_win == per_cu_plain);
+    win = per_cu_win > per_cu_plain;
     per_cu = win ? per_cu_win : per_cu_plain;
   } else {
-    rc = occupancy(ctx, kfns[kind][ctx->stats_on][0][pair][glossy][help], lds_plain, &per_cu);
+    rc = occupancy(ctx, kfns[kind][ctx->stats_on][0][pair][glossy], lds_plain, &per_cu);
     if (rc) return rc;
   }
   const size_t lds = win ? lds_win : lds_plain;
-  const void *kfn = kfns[kind][ctx->stats_on][win][pair][glossy][help];
+  const void *kfn = kfns[kind][ctx->stats_on][win][pair][glossy];
   A.stack_depth = win ? kStackWindow : depth_entries;  // the uniforms and material table follow the stack in LDS
   A.spill_stride = win ? std::max(0, depth_entries - kStackWindow) : 0;
-  A.coop_off = (int32_t)(win ? base_win : base_plain);
-  A.coop_nmax = win ? coop_win : coop_plain;
   const int64_t grid = std::max<int64_t>(1, std::min<int64_t>(tiles, (int64_t)std::max(per_cu, 1) * ctx->n_cu));
   const int64_t spill_need = win ? grid * 64 * (int64_t)A.spill_stride : 0;
   if (win && spill_need > ctx->spill_cap) {
@@ -3209,8 +2798,6 @@ int mcpt_render_frames(mcpt_ctx *ctx, const mcpt_scene *scene, const mcpt_camera
   ctx->last.frames_per_block = fpl_head;
   ctx->last.stack_window = win ? 1 : 0;
   ctx->last.quantized = kind == 2 ? 1 : 0;
-  ctx->last.t_helpers = help == 1 ? 1 : 0;
-  ctx->last.merged_gather = help == 2 ? 1 : 0;
   ctx->last.workgroups = (int32_t)grid;
   ctx->last.primary_cache = prim_state;
   ctx->last_pending = true;

@@ -51,6 +51,23 @@ def test_lobe_pow_matches_ocml(rnd):
     assert rnd.selfcheck_pow(sorted(ns) + edges) == 0
 
 
+def test_lobe_pow_matches_ocml_exponent_sweep(rnd):
+    """The restatement's whole exponent domain, not only the scenes' Ns: a
+    stratified seeded sweep of y over [0, 65536] (log-uniform over 2^-20..2^16,
+    uniform over [0, 65536], integers and half-integers, the domain's top
+    floats), every float x in (0, 1 + 2^-10] for each: __ocml_pow_f32's bits.
+    A user scene's Ns outside the tested list is covered by the domain
+    argument of mcpt_refmath.h:121-130 and this sweep together."""
+    g = np.random.default_rng(20261018)
+    ys = list(np.float32(2.0) ** g.uniform(-20.0, 16.0, 24).astype(np.float32))
+    ys += list(g.uniform(0.0, 65536.0, 12).astype(np.float32))
+    ys += [float(v) for v in g.integers(1, 65536, 8)] + [float(v) + 0.5 for v in g.integers(1, 65535, 4)]
+    ys += [float(np.nextafter(np.float32(65536.0), np.float32(0.0))), 65535.0, 1.0e-30, 3.0]
+    ys = sorted({float(np.float32(y)) for y in ys})
+    assert all(0.0 <= y <= 65536.0 for y in ys) and len(ys) >= 48
+    assert rnd.selfcheck_pow(ys) == 0
+
+
 @pytest.mark.parametrize("k", list(CAMS))
 def test_rays_equal_golden(rnd, k):
     mine = R.records(rnd.generate_rays(S.parse_camera(CAMS[k]), 64, 48), L.RAY)

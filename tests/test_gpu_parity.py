@@ -776,183 +776,3 @@ def test_handoff_tag_wrap_bitexact(rnd):
         assert_bits_equal(b.hist.cpu().numpy(), rh, "hist vs reference")
         assert_bits_equal(b.seeds_np(), rs, "seeds vs reference")
     dsc.close()
-
-
-@needs_ref
-@pytest.mark.parametrize("name,getter,camjson,depth", [("cbox", scenes.cbox, scenes.CBOX_CAM, 8),
-                                                       ("cbox_diffuse", scenes.cbox_diffuse, scenes.CBOX_CAM, 8),
-                                                       ("mis", scenes.mis, scenes.MIS_CAM, 12),
-                                                       ("dining", scenes.dining, scenes.DINING_CAM, 16)])
-@pytest.mark.parametrize("quantized", [1, 2])
-@pytest.mark.parametrize("window", [2, 1])  # the whole stack in LDS, or the LDS window + global spill (forced)
-def test_t_helpers_bitexact(rnd, name, getter, camjson, depth, quantized, window):
-    """T-phase helpers (mcpt_tuning.t_helpers 2): lanes not stepping in a T
-    phase step their partner lane's stack-top node and push onto the
-    partner's stack (its LDS column, or its window and global spill), with
-    the partner's pruning bound.  The candidate set and the order-free
-    t1 / t2 rule are unchanged, so images, counts and seed chains still
-    match the reference kernels bit for bit; the counters show helpers ran."""
-    rnd.set_tuning(t_helpers=2, quantized=quantized, stack_window=window)
-    stats = window == 2 and quantized == 2
-    if stats:
-        rnd.set_stats(True)
-    try:
-        (h_, c_, s_), (rh, rc, rs) = _render_both(rnd, getter(), camjson, 64, 64, depth, 4, 4)
-        st = rnd.stats()
-    finally:
-        rnd.set_stats(False)
-        rnd.set_tuning()
-    assert st["t_helpers"] == 1 and st["stack_window"] == (1 if window == 1 else 0)
-    if stats:
-        assert 0 < st["helped_steps"] < st["node_visits"]
-    assert_bits_equal(c_, rc, "count")
-    assert_bits_equal(s_, rs, "seeds")
-    assert_bits_equal(h_, rh, "hist")
-
-
-@needs_ref
-@pytest.mark.parametrize("name,offset,camjson", NEAR_TIES)
-def test_t_helpers_near_ties_bitexact(rnd, name, offset, camjson):
-    """Helpers with twin triangles less than EPS apart: the ambiguous rays
-    still fall back to the (never helped) reference-order search."""
-    data = scenes.near_ties(name, offset)
-    rnd.set_stats(True)
-    rnd.set_tuning(t_helpers=2)
-    try:
-        (h_, c_, s_), (rh, rc, rs) = _render_both(rnd, data, camjson, 64, 64, 6, 4, 4)
-        st = rnd.stats()
-    finally:
-        rnd.set_stats(False)
-        rnd.set_tuning()
-    assert_bits_equal(c_, rc, "count")
-    assert_bits_equal(s_, rs, "seeds")
-    assert_bits_equal(h_, rh, "hist")
-    assert st["order_fallbacks"] > 0 and st["helped_steps"] > 0
-
-
-@needs_ref
-@pytest.mark.parametrize("quantized", [1, 2])
-def test_t_helpers_random_mesh_bitexact(rnd, quantized):
-    """Helpers on C5's deep random-soup tree (500 K triangles): the deepest
-    stacks, the window stack on auto, 2-frame blocks handed between lanes."""
-    data = _c5_small()
-    rnd.set_tuning(t_helpers=2, quantized=quantized)
-    try:
-        (h_, c_, s_), (rh, rc, rs) = _render_both(rnd, data, S.RANDOM_MESH_CAMERA, 64, 64, 8, 5, 4,
-                                                  frames_per_launch=2)
-        assert rnd.stats()["t_helpers"] == 1
-    finally:
-        rnd.set_tuning()
-    assert_bits_equal(c_, rc, "count")
-    assert_bits_equal(s_, rs, "seeds")
-    assert_bits_equal(h_, rh, "hist")
-
-
-def test_t_helpers_full_size_same_bits(rnd):
-    """Size-independent property at C2's size: helpers on and off give the
-    same image on the whole 1024x1024 image and on a strong-scaled 8-rank
-    share (sparse waves, where most lanes are free to help)."""
-    data, cam = scenes.cbox_diffuse(), S.parse_camera(scenes.CBOX_CAM)
-    w = h = 1024
-    seeds = R.default_seeds(w * h)
-    dsc = rnd.upload(data)
-    try:
-        for stripes in (1, 8):
-            outs = []
-            for th in (1, 2):
-                rnd.set_tuning(t_helpers=th)
-                st = rnd.new_state(w, h, seeds)
-                rnd.render_frames(dsc, cam, st, 8, 1 << 20, 12, stripe_rows=16, stripe_index=stripes - 1,
-                                  stripe_count=stripes)
-                torch.cuda.synchronize()
-                assert rnd.stats()["t_helpers"] == (1 if th == 2 else 0)
-                outs.append((st.hist.cpu().numpy(), st.count.cpu().numpy(), st.seeds_np()))
-            for a, b, what in zip(outs[0], outs[1], ("hist", "count", "seeds")):
-                assert_bits_equal(a, b, "%s / %d stripes" % (what, stripes))
-    finally:
-        rnd.set_tuning()
-        dsc.close()
-
-
-@needs_ref
-@pytest.mark.parametrize("name,getter,camjson,depth", [("cbox", scenes.cbox, scenes.CBOX_CAM, 8),
-                                                       ("cbox_diffuse", scenes.cbox_diffuse, scenes.CBOX_CAM, 8),
-                                                       ("mis", scenes.mis, scenes.MIS_CAM, 12),
-                                                       ("dining", scenes.dining, scenes.DINING_CAM, 16)])
-@pytest.mark.parametrize("schedule", [L.SCHED_SINGLE, L.SCHED_PAIRED])
-@pytest.mark.parametrize("window", [2, 1])
-def test_merged_gather_bitexact(rnd, name, getter, camjson, depth, schedule, window):
-    """Merged T / L gathers (mcpt_tuning.merged_gather 2, the 128-B search
-    tree): a lane holding a leaf at the iteration's start fetches its
-    triangle (or the paired two) in the T phase's load instructions, and a
-    T step that ends on a leaf is tested next iteration.  Every lane's
-    sequence of operations is the same, so images, counts and seed chains
-    match the reference kernels bit for bit, with either leaf schedule and
-    stack layout, counters on and off."""
-    rnd.set_tuning(merged_gather=2, quantized=2, stack_window=window)
-    stats = window == 2
-    if stats:
-        rnd.set_stats(True)
-    try:
-        (h_, c_, s_), (rh, rc, rs) = _render_both(rnd, getter(), camjson, 64, 64, depth, 4, 4, schedule=schedule)
-        st = rnd.stats()
-    finally:
-        rnd.set_stats(False)
-        rnd.set_tuning()
-    assert st["merged_gather"] == 1 and st["quantized"] == 0 and st["stack_window"] == (1 if window == 1 else 0)
-    if stats:
-        assert st["tri_tests"] > 0 and st["wave_leaf_phases"] > 0
-    assert_bits_equal(c_, rc, "count")
-    assert_bits_equal(s_, rs, "seeds")
-    assert_bits_equal(h_, rh, "hist")
-
-
-@needs_ref
-@pytest.mark.parametrize("name,offset,camjson", NEAR_TIES)
-def test_merged_gather_near_ties_bitexact(rnd, name, offset, camjson):
-    """Merged gathers with twin triangles less than EPS apart: the
-    reference-order fallback runs through the merged phase too."""
-    data = scenes.near_ties(name, offset)
-    rnd.set_stats(True)
-    rnd.set_tuning(merged_gather=2, quantized=2)
-    try:
-        (h_, c_, s_), (rh, rc, rs) = _render_both(rnd, data, camjson, 64, 64, 6, 4, 4)
-        st = rnd.stats()
-    finally:
-        rnd.set_stats(False)
-        rnd.set_tuning()
-    assert_bits_equal(c_, rc, "count")
-    assert_bits_equal(s_, rs, "seeds")
-    assert_bits_equal(h_, rh, "hist")
-    assert st["order_fallbacks"] > 0 and st["merged_gather"] == 1
-
-
-def test_merged_gather_full_size_same_bits(rnd):
-    """Size-independent property at C2's and C4's sizes: merged gathers on
-    and off give the same image on the whole image and on an 8-rank share;
-    the quantized tree (C5's) keeps the plain phases."""
-    for getter, camjson, depth, w, h, frames in ((scenes.cbox_diffuse, scenes.CBOX_CAM, 8, 1024, 1024, 12),
-                                                 (scenes.dining, scenes.DINING_CAM, 16, 1920, 1080, 3)):
-        data, cam = getter(), S.parse_camera(camjson)
-        seeds = R.default_seeds(w * h)
-        dsc = rnd.upload(data)
-        try:
-            for stripes in (1, 8):
-                outs = []
-                for mg in (1, 2):
-                    rnd.set_tuning(merged_gather=mg)
-                    st = rnd.new_state(w, h, seeds)
-                    rnd.render_frames(dsc, cam, st, depth, 1 << 20, frames, stripe_rows=16, stripe_index=stripes - 1,
-                                      stripe_count=stripes)
-                    torch.cuda.synchronize()
-                    assert rnd.stats()["merged_gather"] == (1 if mg == 2 else 0)
-                    outs.append((st.hist.cpu().numpy(), st.count.cpu().numpy(), st.seeds_np()))
-                for a, b, what in zip(outs[0], outs[1], ("hist", "count", "seeds")):
-                    assert_bits_equal(a, b, "%s / %d stripes" % (what, stripes))
-            rnd.set_tuning(merged_gather=2, quantized=1)
-            st = rnd.new_state(64, 64)
-            rnd.render_frames(dsc, cam, st, depth, 4, 1)
-            assert rnd.stats()["merged_gather"] == 0 and rnd.stats()["quantized"] == 1
-        finally:
-            rnd.set_tuning()
-            dsc.close()

@@ -28,7 +28,10 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 PROF = os.path.join(ROOT, "profiles")
 RENDER_KERNELS = re.compile(r"k_render|k_primary|k_tile_")
-NON_PRIM = re.compile(r"k_render<[^>]*, false, (false|true)(, [a-z0-9]+)?>")
+# k_render<MODE, STATS, WIN, PAIR, Q-or-node-format, PRIM, G[, VAR]>: PRIM (the
+# primary-hit pass) anchored by position, so a G or VAR argument never reads as it
+NON_PRIM = re.compile(r"k_render<-?\d+, (?:false|true), (?:false|true), (?:false|true), (?:false|true|\d+), false, "
+                      r"(?:false|true)(?:, \d+)?>")
 
 
 def _rows(text):
@@ -72,14 +75,20 @@ def trim_file(path):
     if kind == "kernel_trace":
         keep = [r for r in rows if RENDER_KERNELS.search(r.get("Kernel_Name", ""))]
     else:
-        kernel = None
         summ = os.path.join(os.path.dirname(path), tag + "_summary.json")
         if os.path.exists(summ):
+            # a summary names the timed kernel: trim to it, or not at all
             try:
                 kernel = json.load(open(summ)).get("kernel")
             except ValueError:
                 kernel = None
-        keep = timed_pmc_rows(rows, kernel) or timed_pmc_rows(rows)
+            if not kernel:
+                return None
+            keep = timed_pmc_rows(rows, kernel)
+        else:
+            keep = timed_pmc_rows(rows)
+        if not keep:
+            return None
     if len(keep) == len(rows):
         return 0
     before = len(text)
