@@ -328,7 +328,9 @@ int mcpt_scene_upload_device(mcpt_ctx *ctx, const mcpt_triangle *tris_dev, int64
 /* A scene's device arrays copied to the host (introspection).  which: 0 the
  * search tree (128-B nodes), 1 its quantized nodes, 2 the reference tree
  * 4-wide, 3 the binary child-box nodes, 4 triangles, 5 quantized-path
- * triangles, 6 int32[4] {stack_depth, stack_depth4, quantized, n_internal}.
+ * triangles, 6 int32[4] {stack_depth, stack_depth4, quantized, n_internal},
+ * 7 the 8-wide search tree (256-B nodes; 0 bytes until a wide_nodes render
+ * built it).
  * *bytes = the size (host NULL: size only).                               */
 int mcpt_scene_read(const mcpt_scene *scene, int32_t which, void *host, int64_t cap, int64_t *bytes);
 

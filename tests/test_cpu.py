@@ -10,6 +10,7 @@ Golden provenance (tools/make_goldens.py):
 import ctypes
 import json
 import os
+import sys
 import re
 
 import numpy as np
@@ -850,3 +851,16 @@ def test_variant_names_map_to_macros(tmp_path):
     macros = [dict(re.findall(r"-D(MCPT_[A-Z_]+)=(\S+)", ln)) for ln in lines]
     assert macros[0] == {"MCPT_WAVES_PER_SIMD": "4", "MCPT_STACK_WINDOW_K": "16", "MCPT_POW_LOBE": "1"}
     assert macros[1] == {"MCPT_WAVES_PER_SIMD": "5", "MCPT_STACK_WINDOW_K": "32", "MCPT_POW_LOBE": "0"}
+
+
+def test_bench_refuses_more_ranks_than_gpus():
+    """bench.py at WORLD_SIZE > visible GPUs (one rank per GPU) exits non-zero
+    before any call that initialises a device, and does not re-launch itself:
+    here (no GPU) two ranks see zero devices."""
+    import subprocess
+    env = dict(os.environ, WORLD_SIZE="2", RANK="0", LOCAL_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT="29555")
+    env.pop("MCPT_BENCH_SHARED_GPU", None)
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "2", "--warmup", "1"],
+                       cwd=ROOT, env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 3, r.stderr[-2000:]
+    assert "needs 2 visible GPUs" in r.stderr and not r.stdout.strip()

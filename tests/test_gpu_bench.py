@@ -54,6 +54,12 @@ def test_bench_two_ranks_rehearsal():
     assert j["image_reduce_ms"] is not None and j["image_reduce_ms"] > 0  # the final image reduce ran
     # the host dump (device-to-host copy of rank 0's image state), timed outside value
     assert j["host_dump"]["bytes"] == 1024 * 2048 * 24 and j["host_dump"]["value_with_dump_per_call"] < j["value"]
+    # the strong-scaling answers at the top level (the scaling record's reader):
+    # the fixed 1024x1024 image, and C4's 1920x1080 image striped over the ranks
+    assert j["strong_speedup_vs_1gpu"] == s["speedup_vs_1gpu"] > 0
+    c4 = j["c4_strong_scaling"]
+    assert c4["image"] == [1920, 1080] and len(c4["share_ms_per_rank"]) == 2 and c4["one_gpu_ms"] > 0
+    assert j["c4_strong_speedup_vs_1gpu"] == c4["speedup_vs_1gpu"] > 0
 
 
 def test_bench_c4_strong_two_ranks_rehearsal():
@@ -69,6 +75,7 @@ def test_bench_c4_strong_two_ranks_rehearsal():
     assert s["image"] == [1920, 1080] and s["value"] == j["value"]
     assert s["one_gpu_ms"] > 0 and s["speedup_vs_1gpu"] > 0 and len(s["share_ms_per_rank"]) == 2
     assert j["image_reduce_ms"] is not None
+    assert j["strong_speedup_vs_1gpu"] == j["c4_strong_speedup_vs_1gpu"] == s["speedup_vs_1gpu"]
 
 
 def test_bench_default_line():

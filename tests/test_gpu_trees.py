@@ -1,0 +1,69 @@
+"""How much of "same scene, same output" rests on the restated treelet tree.
+
+The reference renders over HLBVH<CPU>::build restructured by its GPU treelet
+kernel (scenebuild.cpp:87-95; treeletBVH.cl does not compile here, so that
+tree comes from our restatement).  The plain HLBVH, which the
+product also builds and which compiles-equivalent code pins, is the other
+tree.  For C1 and C3 this module renders over BOTH trees with the reference's
+own kernels and with the HIP path: each pair must be bit-exact, and the
+number of pixels whose reference images differ between the two trees is the
+share of the output that depends on which tree the reference traverses (only
+its left-first tie winners among hits less than EPS apart can differ).
+"""
+import json
+
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+
+pytestmark = pytest.mark.gpu
+
+from montecarlopathtracing_amd import render as R  # noqa: E402
+
+from . import scenes  # noqa: E402
+from .test_gpu_parity import _render_both, assert_bits_equal, needs_ref  # noqa: E402
+
+# (scene, camera, width, height, depth, frames, MAX_ATTEMPT): C1 is config.json's
+# configid 2 at its own size; C3 is veach_mis at C3's size and depth, 4 frames
+CASES = {"C1": (scenes.cbox, scenes.CBOX_CAM, 256, 256, 4, 16, 16),
+         "C3": (scenes.mis, scenes.MIS_CAM, 1024, 1024, 12, 4, 1 << 20)}
+
+
+@pytest.fixture(scope="module")
+def rnd():
+    return R.Renderer(0)
+
+
+def tree_exposure(rnd, case):
+    """Render `case` over the plain HLBVH and over the GPU-treelet tree with
+    the reference kernels and the HIP path; assert each pair bit-exact; return
+    the pixels whose reference images differ between the trees."""
+    getter, camjson, w, h, depth, frames, attempt = CASES[case]
+    plain = getter()
+    trees = {"hlbvh": plain, "treelet_gpu": plain.with_nodes(R.treelet_gpu_device(plain.nodes))}
+    refs = {}
+    for name, data in trees.items():
+        (h_, c_, s_), (rh, rc, rs) = _render_both(rnd, data, camjson, w, h, depth, frames, attempt)
+        assert_bits_equal(c_, rc, "%s/%s count" % (case, name))
+        assert_bits_equal(s_, rs, "%s/%s seeds" % (case, name))
+        assert_bits_equal(h_, rh, "%s/%s hist" % (case, name))
+        refs[name] = (rh, rc, rs)
+    (ha, ca, sa), (hb, cb, sb) = refs["hlbvh"], refs["treelet_gpu"]
+    px = np.any(np.ascontiguousarray(ha).view(np.uint32).reshape(w * h, -1) !=
+                np.ascontiguousarray(hb).view(np.uint32).reshape(w * h, -1), axis=1) | (ca != cb) | (sa != sb)
+    return {"case": case, "image": [w, h], "depth": depth, "frames": frames, "pixels": w * h,
+            "pixels_differing_between_trees": int(px.sum()), "frac": round(float(px.mean()), 6),
+            "mean_abs_diff": float(np.abs(ha[:, :3].astype(np.float64) - hb[:, :3]).mean()),
+            "bitexact_vs_reference": {"hlbvh": True, "treelet_gpu": True}}
+
+
+@needs_ref
+@pytest.mark.parametrize("case", sorted(CASES))
+def test_both_trees_bitexact_and_exposure(rnd, case):
+    """Both trees, both implementations, bit for bit; the exposure is
+    reported (and bounded: the trees hold the same triangles, so only near
+    ties can part them)."""
+    r = tree_exposure(rnd, case)
+    print(json.dumps(r))
+    assert 0 <= r["pixels_differing_between_trees"] < r["pixels"]

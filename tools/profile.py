@@ -341,6 +341,9 @@ def td_model(src, ctr, n_cu, cycles):
                     "1-lane gather costs ~18 cycles, a 64-lane one on 64 lines ~65), so SIMT efficiency moves it"}
 
 
+B_LINE_MICROBENCH = 0.7435  # tools/mb/td_lanes.hip: TD cycles per L1 line a gather touches (r04a_tdcal)
+
+
 def refit():
     """The TD floor model, fitted on every committed profile (VERDICT r4 next
     3): TD_TD_BUSY_sum = a x SQ_INSTS_VMEM_RD + b x L1-hit line accesses +
@@ -366,12 +369,25 @@ def refit():
     y = np.array([c["TD_TD_BUSY_sum"] for _, _, c in rows])
     (a, b, cm), _ = nnls(X, y)
     ratio = {t: round(float(p / m), 4) for (t, _, _), p, m in zip(rows, X @ np.array([a, b, cm]), y)}
+    # the free fit is degenerate: across these profiles (one kernel family)
+    # gather instructions and line accesses move together (collinear), and NNLS
+    # puts the line term at b = 0.  The TD microbenchmark measures the per-line
+    # cost directly (tools/mb/td_lanes.hip: 0.74 cycle per line, 64 lines 65.0
+    # cycles, 1 line 18.0), so the second fit holds b there and fits a and c
+    b_mb = B_LINE_MICROBENCH
+    (a2, c2), _ = nnls(X[:, [0, 2]], y - b_mb * X[:, 1])
+    ratio2 = {t: round(float(p / m), 4) for (t, _, _), p, m in zip(rows, X @ np.array([a2, b_mb, c2]), y)}
+    corr = float(np.corrcoef(X[:, 0], X[:, 1])[0, 1])
     by_wl = {}
     for (t, wl, _), r in zip(rows, ratio.values()):
         by_wl.setdefault(wl, []).append(r)
     fit = {"a_cycles_per_gather_inst": round(float(a), 4), "b_cycles_per_l1_hit_line": round(float(b), 4),
            "c_cycles_per_l2_request": round(float(cm), 4), "profiles": len(rows),
            "modelled_over_measured_busy": ratio,
+           "corr_gather_insts_vs_l1_hit_lines": round(corr, 4),
+           "b_fixed": {"a_cycles_per_gather_inst": round(float(a2), 4), "b_cycles_per_l1_hit_line": b_mb,
+                       "c_cycles_per_l2_request": round(float(c2), 4), "modelled_over_measured_busy": ratio2,
+                       "note": "b held at the microbenchmark's per-line cost; a, c by NNLS on the rest"},
            "range_by_workload": {k: [min(v), max(v)] for k, v in sorted(by_wl.items())},
            "note": "TD_TD_BUSY_sum (busy cycles summed over CUs) = a x SQ_INSTS_VMEM_RD + b x (TCP_TOTAL_CACHE_ACCESSES_sum "
                    "- TCP_TCC_READ_REQ_sum) + c x TCP_TCC_READ_REQ_sum, non-negative least squares over the timed launch of "
@@ -391,9 +407,12 @@ def refit():
         n_cu, cyc = s.get("cus", N_CU_DEFAULT), s["kernel_cycles"]
         vm, acc, l2 = c["SQ_INSTS_VMEM_RD"], c["TCP_TOTAL_CACHE_ACCESSES_sum"], c["TCP_TCC_READ_REQ_sum"]
         floor = a * vm + b * (acc - l2) + cm * l2
+        floor2 = a2 * vm + b_mb * (acc - l2) + c2 * l2
         e["td_fit"] = {"floor_cycles_per_cu": round(float(floor / n_cu), 1), "kernel_cycles": cyc,
                        "model_frac": round(float(floor / n_cu / cyc), 4),
                        "inst_term_share": round(float(a * vm / max(floor, 1.0)), 4),
+                       "model_frac_b_fixed": round(float(floor2 / n_cu / cyc), 4),
+                       "inst_term_share_b_fixed": round(float(a2 * vm / max(floor2, 1.0)), 4),
                        "td_busy_per_cycle": round(c["TD_TD_BUSY_sum"] / (n_cu * cyc), 4),
                        "vmem_rd_insts": vm, "l1_accesses": acc, "l2_requests": l2,
                        "l1_lines_per_vmem_rd_inst": round(acc / max(vm, 1), 2), "fit": "profiles/td_floor_fit.json"}
