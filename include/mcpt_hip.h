@@ -176,8 +176,6 @@ typedef struct mcpt_stats {
                                        primary hits; 2: it computed them too  */
   double   primary_ms;              /* primary_cache 2: device time of the
                                        primary-hit pass (part of kernel_ms)   */
-  int32_t  wide_nodes;              /* 1: the last call searched the 8-wide
-                                       search tree (EXACT mode)               */
 } mcpt_stats;
 
 /* Launch-plan knobs of the fused kernel (speed only: every setting gives the
@@ -236,11 +234,6 @@ typedef struct mcpt_tuning {
                                consecutive slots are one 8x8 tile), 2 spread
                                (they are one pixel of each of 64 tiles, so one
                                tile's dear pixels run in different waves)      */
-  int32_t wide_nodes;       /* EXACT search tree width: 0 auto (the 4-wide
-                               tree), 1 the 4-wide tree (128-B or quantized
-                               nodes, `quantized`), 2 the 8-wide tree (256-B
-                               nodes, fewer dependent node steps per ray;
-                               DESIGN.md §3.3)                                  */
 } mcpt_tuning;
 
 /* ------------------------------------------------------- version / errors */
@@ -248,10 +241,9 @@ typedef struct mcpt_tuning {
  * passed across the boundary changes size or layout, or an entry point its
  * arguments (3: mcpt_tuning's tile_order / pixel_spread,
  * mcpt_set_pixel_segments' capacity; 4: the rejected T-phase-helper and
- * merged-gather knobs and counters removed from mcpt_tuning / mcpt_stats,
- * `wide_nodes` added to both).  A binding checks mcpt_abi_version() ==
- * MCPT_ABI_VERSION once at load and refuses a library built from another
- * header.                                                                */
+ * merged-gather knobs and counters removed from mcpt_tuning / mcpt_stats).
+ * A binding checks mcpt_abi_version() == MCPT_ABI_VERSION once at load and
+ * refuses a library built from another header.                           */
 #define MCPT_ABI_VERSION 4
 int32_t mcpt_abi_version(void);
 const char *mcpt_version(void);
@@ -328,9 +320,7 @@ int mcpt_scene_upload_device(mcpt_ctx *ctx, const mcpt_triangle *tris_dev, int64
 /* A scene's device arrays copied to the host (introspection).  which: 0 the
  * search tree (128-B nodes), 1 its quantized nodes, 2 the reference tree
  * 4-wide, 3 the binary child-box nodes, 4 triangles, 5 quantized-path
- * triangles, 6 int32[4] {stack_depth, stack_depth4, quantized, n_internal},
- * 7 the 8-wide search tree (256-B nodes; 0 bytes until a wide_nodes render
- * built it).
+ * triangles, 6 int32[4] {stack_depth, stack_depth4, quantized, n_internal}.
  * *bytes = the size (host NULL: size only).                               */
 int mcpt_scene_read(const mcpt_scene *scene, int32_t which, void *host, int64_t cap, int64_t *bytes);
 

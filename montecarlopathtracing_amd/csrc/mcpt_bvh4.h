@@ -58,26 +58,4 @@ static_assert(sizeof(Node4Q) == 64, "four 16-B loads");
 // (the scene then keeps the 128-B nodes).
 int quantize_node4(const Node4Rec &in, Node4Q &out);
 
-// 256-B 8-wide node of the same search tree (DevNode8): slot k's box is
-// q[6k..6k+5] in Node4Rec's plane order, link as Node4Rec's.  Fourteen 16-B
-// gathers per step (the last 32 B are padding: two 128-B lines per node).
-struct Node8Rec {
-  float q[48];
-  int32_t link[8];
-  float pad[8];
-};
-static_assert(sizeof(Node8Rec) == 256, "DevNode8 layout");
-
-// The 4-wide search tree widened to 8 slots: an SAH-optimal choice of which
-// internal slots of each 4-wide node to open (splice their slots in place), a
-// dynamic programme over the 4-wide tree with build_sah4's costs.  Every slot
-// keeps the 4-wide slot's box bit for bit, so each leaf keeps the reference
-// leaf's own box and every internal box is still a union of leaf boxes
-// (DESIGN.md §3.3); slots stay in the 4-wide tree's left-to-right order.
-// A pure function of the 4-wide tree: both upload paths, whose 4-wide trees
-// are byte-identical, get the same 8-wide bytes.  Nodes in depth-first
-// preorder (root = 0); *stack_need as build_sah4's.  Returns 0, or -1 for an
-// empty input.
-int widen_sah8(const std::vector<Node4Rec> &in, std::vector<Node8Rec> &out, int32_t *stack_need);
-
 }  // namespace mcpt

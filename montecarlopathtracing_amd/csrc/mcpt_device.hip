@@ -113,15 +113,6 @@ struct __attribute__((aligned(16))) DevNode4Q {
   int32_t link[4];
 };
 static_assert(sizeof(DevNode4Q) == 64 && sizeof(DevNode4Q) == sizeof(mcpt::Node4Q), "64-B quantized node");
-// 8-wide node of the same search tree (mcpt::widen_sah8): eight slot boxes in
-// DevNode4's packed pair order, then the eight links; 224 B read as fourteen
-// 16-B gathers, padded to two 128-B lines.
-struct __attribute__((aligned(16))) DevNode8 {
-  f4 q[12];
-  int32_t link[8];
-  f4 pad[2];
-};
-static_assert(sizeof(DevNode8) == 256 && sizeof(DevNode8) == sizeof(mcpt::Node8Rec), "256-B 8-wide node");
 // Triangle record of the quantized path: the raw vertices (so the L phase can
 // rebuild the reference leaf's exact box, hlbvh.cpp:97-100) with the three
 // triangle-only Cramer minors in .w, then the packed normal / material id.
@@ -144,8 +135,6 @@ struct SceneView {
   const DevTri *tris;
   const DevNode4Q *near4q;  // near4 quantized (nullptr: the scene keeps the 128-B nodes only)
   const DevTriQ *triq;      // triangles for the quantized path
-  const DevNode8 *near8;    // the search tree 8-wide (nullptr until a call asks for it)
-  int32_t n_near8;
   const mcpt_material *mats;
   f4 root_min, root_max;
   int32_t root_leaf;  // >= 0: single-triangle scene, root is that leaf
@@ -169,11 +158,6 @@ struct mcpt_scene {
   int32_t n_mats = 0;
   int32_t stack_depth = 1;
   bool has_glossy = true;  // any GLOSSY material: k_render's glossy-lobe shading path
-  int32_t stack_depth_ref4 = 1;  // the reference tree's 4-wide stack need alone
-  // the 8-wide search tree: built from near4 on first use (mcpt::widen_sah8);
-  // its stack bound includes the reference tree's (the fallback search)
-  DevNode8 *near8 = nullptr;
-  int32_t stack_depth8 = 1;
   SceneView view;
 };
 
@@ -432,44 +416,6 @@ __device__ inline int32_t step4q(f4 q0, f4 q1, f4 q2, f4 q3, f4 q4, f4 q5, int32
   if (h2 && sel != 2) stk.push(sp, l2);
   if (h1 && sel != 1) stk.push(sp, l1);
   if (h0 && sel != 0) stk.push(sp, l0);
-  return nxt;
-}
-
-// One 8-wide node of the search tree, nearest first: step4q's rule over eight
-// slots (the passing slot with the smallest entry distance is entered, ties
-// to the lower slot; the others are pushed so they pop in slot order).  The
-// search tree only: the reference tree stays 4-wide (left-first fallback).
-template <bool PRUNE, class Stk>
-__device__ inline int32_t step8(const DevNode8 &N, f3 o, f3 rinv, float tmin, float lim, const Stk &stk, int &sp,
-                                uint32_t &nodes_ctr) {
-  f4 q[12];
-#pragma unroll
-  for (int k = 0; k < 12; ++k) q[k] = N.q[k];
-  int32_t l[8];
-#pragma unroll
-  for (int k = 0; k < 8; ++k) l[k] = N.link[k];
-  BoxT b[8];
-#pragma unroll
-  for (int k = 0; k < 4; ++k) {  // slots 2k, 2k+1 in q[3k .. 3k+2]
-    b[2 * k] = slab_pairs(q[3 * k].xy, q[3 * k].zw, q[3 * k + 1].xy, o, rinv);
-    b[2 * k + 1] = slab_pairs(q[3 * k + 1].zw, q[3 * k + 2].xy, q[3 * k + 2].zw, o, rinv);
-  }
-  bool h[8];
-#pragma unroll
-  for (int k = 0; k < 8; ++k) {
-    h[k] = slab_pass(b[k], tmin) && l[k] != kEmptySlot;
-    if (PRUNE) h[k] = h[k] && !(b[k].tnear > lim);
-  }
-  nodes_ctr++;
-  int32_t nxt = kPop;
-  int sel = 8;
-  float kb = __builtin_inff();
-#pragma unroll
-  for (int k = 7; k >= 0; --k)
-    if (h[k] && !(b[k].tnear > kb)) kb = b[k].tnear, nxt = l[k], sel = k;
-#pragma unroll
-  for (int k = 7; k >= 0; --k)
-    if (h[k] && sel != k) stk.push(sp, l[k]);
   return nxt;
 }
 
@@ -916,14 +862,11 @@ __device__ inline uint32_t queue_items(uint32_t x, uint32_t n_tiles, uint32_t nq
 // PRIM: the primary-hit pass (PrimHit) run by the same machine: one frame,
 // no pixel state; a lane traces its pixel's primary ray, stores the closest
 // hit at the S phase instead of shading, and takes the next pixel.
-// NF: the search tree's node format, 0 the 128-B 4-wide nodes, 1 their
-// quantized 64-B form, 2 the 256-B 8-wide nodes
-template <int MODE, bool STATS, bool WIN, bool PAIR, int NF, bool PRIM = false, bool G = true>
+template <int MODE, bool STATS, bool WIN, bool PAIR, bool Q, bool PRIM = false, bool G = true>
 __global__ void __launch_bounds__(64, MCPT_WAVES_PER_SIMD) k_render(RenderArgs A) {
-  constexpr bool Q = NF == 1, W8 = NF == 2;
   constexpr bool PRUNE = MODE != MCPT_MODE_NOPRUNE;
   constexpr bool LIT = MODE == MCPT_MODE_NOPRUNE;
-  static_assert(!((Q || W8) && LIT), "the quantized and 8-wide search trees are EXACT-mode structures");
+  static_assert(!(Q && LIT), "the quantized search tree is an EXACT-mode structure");
   extern __shared__ int32_t lds_stack[];
   const int lane = threadIdx.x;
   // the whole stack in LDS, or its top kStackWindow entries (deep trees, where
@@ -1271,15 +1214,6 @@ __global__ void __launch_bounds__(64, MCPT_WAVES_PER_SIMD) k_render(RenderArgs A
             }
             cur = step4q<PRUNE>(q0, q1, q2, q3, q4, q5, l0, l1, l2, l3, o.xyz, rinv, kTmin, best_t + S.prune_margin,
                                 !ref, sk, sp, ctr);
-            if (!MCPT_DCHECK(sp <= stack_cap, 0)) sp = stack_cap;
-          } else {
-            cur = kPop;
-          }
-          if (STATS) n_nodes += ctr;
-        } else if (W8 && !ref) {  // EXACT: the 8-wide SAH tree nearest-first (14 loads)
-          uint32_t ctr = 0;
-          if (MCPT_DCHECK(cur < S.n_near8, 1)) {
-            cur = step8<PRUNE>(S.near8[cur], o.xyz, rinv, kTmin, best_t + S.prune_margin, sk, sp, ctr);
             if (!MCPT_DCHECK(sp <= stack_cap, 0)) sp = stack_cap;
           } else {
             cur = kPop;
@@ -1990,7 +1924,7 @@ int mcpt_set_tuning(mcpt_ctx *c, const mcpt_tuning *t) {
             t->primary_cache < 0 || t->primary_cache > 2 || t->lds_pad < 0 || t->lds_pad > 65536 ||
             t->queue_chunk > 4096 || t->leaf_threshold > 64 || t->shade_threshold > 64 || t->fetch_threshold > 64 ||
             t->last_block_frames < -1 || t->tile_order < 0 || t->tile_order > 2 || t->pixel_spread < 0 ||
-            t->pixel_spread > 2 || t->wide_nodes < 0 || t->wide_nodes > 2))
+            t->pixel_spread > 2))
     return mcpt::fail(MCPT_ERR_ARG, "set_tuning: value out of range");
   if (t)
     c->tune = *t;
@@ -2198,7 +2132,6 @@ int mcpt_scene_upload(mcpt_ctx *ctx, const mcpt_triangle *tris, int64_t n_tris, 
     near.resize(1);
     std::memset(near.data(), 0, sizeof(mcpt::Node4Rec));
   }
-  const int32_t depth_ref4 = depth4;
   depth4 = std::max(depth4, depth_near);
   if (depth4 > 192) return mcpt::fail(MCPT_ERR_LIMIT, "scene_upload: 4-wide stack too deep");
   std::vector<DevTri> dt(n);
@@ -2291,7 +2224,6 @@ int mcpt_scene_upload(mcpt_ctx *ctx, const mcpt_triangle *tris, int64_t n_tris, 
   for (int32_t k = 0; k < n_mats; ++k) s->has_glossy |= mats[k].type == MCPT_GLOSSY;
   s->stack_depth = std::max(depth, 1);
   s->stack_depth4 = depth4;
-  s->stack_depth_ref4 = depth_ref4;
   SceneView &v = s->view;
   v.n_near4 = (int32_t)near.size();
   v.n_nodes4 = (int32_t)dn4.size();
@@ -2357,7 +2289,6 @@ int mcpt_scene_upload_device(mcpt_ctx *ctx, const mcpt_triangle *tris_dev, int64
   for (int32_t k = 0; k < n_mats; ++k) s->has_glossy |= mats[k].type == MCPT_GLOSSY;
   s->stack_depth = std::max(D.stack_depth, 1);
   s->stack_depth4 = D.depth4;
-  s->stack_depth_ref4 = D.depth_ref4;
   float dx = root.bbmax[0] - root.bbmin[0], dy = root.bbmax[1] - root.bbmin[1], dz = root.bbmax[2] - root.bbmin[2];
   float diag = std::sqrt(dx * dx + dy * dy + dz * dz);
   SceneView &v = s->view;
@@ -2398,7 +2329,6 @@ int mcpt_scene_read(const mcpt_scene *s, int32_t which, void *host, int64_t cap,
     case 4: src = s->tris, n = s->n_tris * (int64_t)sizeof(DevTri); break;
     case 5: src = s->triq, n = s->triq ? s->n_tris * (int64_t)sizeof(DevTriQ) : 0; break;
     case 6: n = sizeof(meta); break;
-    case 7: src = s->near8, n = s->near8 ? (int64_t)s->view.n_near8 * (int64_t)sizeof(DevNode8) : 0; break;
     default: return mcpt::fail(MCPT_ERR_ARG, "scene_read: unknown array");
   }
   *bytes = n;
@@ -2421,42 +2351,9 @@ int mcpt_scene_destroy(mcpt_scene *s) {
   if (s->near4) (void)hipFree(s->near4);
   if (s->tris) (void)hipFree(s->tris);
   if (s->near4q) (void)hipFree(s->near4q);
-  if (s->near8) (void)hipFree(s->near8);
   if (s->triq) (void)hipFree(s->triq);
   if (s->mats) (void)hipFree(s->mats);
   delete s;
-  return MCPT_OK;
-}
-
-// The 8-wide search tree (mcpt::widen_sah8), built on first use from the
-// 4-wide tree as it lies in HBM -- so both upload paths, whose 4-wide trees
-// are byte-identical, get the same bytes.  Its stack bound covers the
-// reference tree's too (the 8-wide search falls back to it).
-static int ensure_near8(mcpt_scene *s) {
-  if (s->near8) return MCPT_OK;
-  HIP_OK(hipSetDevice(s->device));
-  std::vector<mcpt::Node8Rec> h8;
-  int32_t need = 1;
-  if (s->view.root_leaf >= 0 || s->n_internal == 0) {  // no nodes: a single-leaf scene (never read)
-    h8.resize(1);
-    std::memset(h8.data(), 0, sizeof(mcpt::Node8Rec));
-  } else {
-    std::vector<mcpt::Node4Rec> h4((size_t)s->view.n_near4);
-    HIP_OK(hipMemcpy(h4.data(), s->near4, h4.size() * sizeof(mcpt::Node4Rec), hipMemcpyDeviceToHost));
-    if (mcpt::widen_sah8(h4, h8, &need) != 0) return mcpt::fail(MCPT_ERR_ARG, "render: 8-wide tree build failed");
-  }
-  const int32_t depth8 = std::max(need, s->stack_depth_ref4);
-  if (depth8 > 192) return mcpt::fail(MCPT_ERR_LIMIT, "render: 8-wide stack too deep");
-  DevNode8 *d = nullptr;
-  HIP_OK(hipMalloc(&d, h8.size() * sizeof(DevNode8)));
-  if (hipMemcpy(d, h8.data(), h8.size() * sizeof(DevNode8), hipMemcpyHostToDevice) != hipSuccess) {
-    (void)hipFree(d);
-    return mcpt::fail(MCPT_ERR_HIP, "render: 8-wide tree upload failed");
-  }
-  s->near8 = d;
-  s->stack_depth8 = depth8;
-  s->view.near8 = d;
-  s->view.n_near8 = (int32_t)h8.size();
   return MCPT_OK;
 }
 
@@ -2525,28 +2422,27 @@ int mcpt_render_frames(mcpt_ctx *ctx, const mcpt_scene *scene, const mcpt_camera
   A.th_fetch = T.fetch_threshold > 0 ? T.fetch_threshold : 1;
   A.n_queues = T.queues > 0 ? (uint32_t)std::min(T.queues, kQueues) : (uint32_t)kQueues;
   const int64_t tiles = (int64_t)A.tiles_x * ((A.local_rows + 7) / 8);
-  int depth_entries = p->mode == MCPT_MODE_NOPRUNE ? scene->stack_depth : scene->stack_depth4;
+  const int depth_entries = p->mode == MCPT_MODE_NOPRUNE ? scene->stack_depth : scene->stack_depth4;
   A.lds_mats = scene->n_mats <= 256 ? 1 : 0;
   const size_t lds_mats = A.lds_mats ? scene->n_mats * sizeof(mcpt_material) : 0;
   // persistent grid: as many 64-lane workgroups as can be resident at once.
   // The stack lives in LDS; when the whole stack would allow fewer resident
   // workgroups than a kStackWindow window does, the windowed kernel runs.
   const bool noprune = p->mode == MCPT_MODE_NOPRUNE;
-  // [kind: 0 EXACT 128-B nodes, 1 NOPRUNE, 2 EXACT quantized, 3 EXACT 8-wide][stats][window][pair][glossy materials]
-#define MCPT_KG(M, ST, W, P, NF) {(const void *)k_render<M, ST, W, P, NF, false, false>, \
-                                  (const void *)k_render<M, ST, W, P, NF, false, true>}
-#define MCPT_KR(M, ST, W, NF) {MCPT_KG(M, ST, W, false, NF), MCPT_KG(M, ST, W, true, NF)}
-#define MCPT_KK(M, NF) {{MCPT_KR(M, false, false, NF), MCPT_KR(M, false, true, NF)}, \
-                        {MCPT_KR(M, true, false, NF), MCPT_KR(M, true, true, NF)}}
-  static const void *const kfns[4][2][2][2][2] = {MCPT_KK(MCPT_MODE_EXACT, 0), MCPT_KK(MCPT_MODE_NOPRUNE, 0),
-                                                  MCPT_KK(MCPT_MODE_EXACT, 1), MCPT_KK(MCPT_MODE_EXACT, 2)};
+  // [kind: 0 EXACT 128-B nodes, 1 NOPRUNE, 2 EXACT quantized][stats][window][pair][glossy materials]
+#define MCPT_KG(M, ST, W, P, QN) {(const void *)k_render<M, ST, W, P, QN, false, false>, \
+                                  (const void *)k_render<M, ST, W, P, QN, false, true>}
+#define MCPT_KR(M, ST, W, QN) {MCPT_KG(M, ST, W, false, QN), MCPT_KG(M, ST, W, true, QN)}
+#define MCPT_KK(M, QN) {{MCPT_KR(M, false, false, QN), MCPT_KR(M, false, true, QN)}, \
+                        {MCPT_KR(M, true, false, QN), MCPT_KR(M, true, true, QN)}}
+  static const void *const kfns[3][2][2][2][2] = {MCPT_KK(MCPT_MODE_EXACT, false), MCPT_KK(MCPT_MODE_NOPRUNE, false),
+                                                  MCPT_KK(MCPT_MODE_EXACT, true)};
   // the primary-hit pass: [kind][window][pair], no stats
-#define MCPT_KP(M, W, NF) {(const void *)k_render<M, false, W, false, NF, true, false>, \
-                           (const void *)k_render<M, false, W, true, NF, true, false>}
-  static const void *const kpfns[4][2][2] = {{MCPT_KP(MCPT_MODE_EXACT, false, 0), MCPT_KP(MCPT_MODE_EXACT, true, 0)},
-                                             {MCPT_KP(MCPT_MODE_NOPRUNE, false, 0), MCPT_KP(MCPT_MODE_NOPRUNE, true, 0)},
-                                             {MCPT_KP(MCPT_MODE_EXACT, false, 1), MCPT_KP(MCPT_MODE_EXACT, true, 1)},
-                                             {MCPT_KP(MCPT_MODE_EXACT, false, 2), MCPT_KP(MCPT_MODE_EXACT, true, 2)}};
+#define MCPT_KP(M, W, QN) {(const void *)k_render<M, false, W, false, QN, true, false>, \
+                           (const void *)k_render<M, false, W, true, QN, true, false>}
+  static const void *const kpfns[3][2][2] = {{MCPT_KP(MCPT_MODE_EXACT, false, false), MCPT_KP(MCPT_MODE_EXACT, true, false)},
+                                             {MCPT_KP(MCPT_MODE_NOPRUNE, false, false), MCPT_KP(MCPT_MODE_NOPRUNE, true, false)},
+                                             {MCPT_KP(MCPT_MODE_EXACT, false, true), MCPT_KP(MCPT_MODE_EXACT, true, true)}};
 #undef MCPT_KP
 #undef MCPT_KK
 #undef MCPT_KR
@@ -2556,18 +2452,8 @@ int mcpt_render_frames(mcpt_ctx *ctx, const mcpt_scene *scene, const mcpt_camera
   // gathers pay (C5 -6 %); on cache-resident trees its looser boxes cost more
   // node steps and leaf tests than the saved gathers (C2 +6 %, C3 +11 %;
   // profiles/r02_quant_ab.txt)
-  // the 8-wide search tree: forced (wide_nodes 2; built from the 4-wide one
-  // on first use), otherwise the 4-wide tree (auto: DESIGN.md §3.3)
-  const bool wide = !noprune && T.wide_nodes == 2;
-  if (wide) {
-    rc = ensure_near8(const_cast<mcpt_scene *>(scene));  // the scene's lazily built array (not its contents)
-    if (rc) return rc;
-    A.S = scene->view;
-    depth_entries = scene->stack_depth8;
-  }
-  const bool quant = !wide && scene->near4q &&
-                     (T.quantized == 1 || (T.quantized == 0 && scene->near4_bytes > kQuantAutoBytes));
-  const int kind = noprune ? 1 : (wide ? 3 : (quant ? 2 : 0));
+  const bool quant = scene->near4q && (T.quantized == 1 || (T.quantized == 0 && scene->near4_bytes > kQuantAutoBytes));
+  const int kind = noprune ? 1 : (quant ? 2 : 0);
   const int glossy = scene->has_glossy ? 1 : 0;  // the shading instantiation (speed only: same bits)
   const size_t pad = (size_t)std::max(0, T.lds_pad);
   const size_t lds_plain = (((size_t)depth_entries * 64 * sizeof(int32_t) + sizeof(LdsUniforms) + lds_mats + 15) & ~(size_t)15) + pad;
@@ -2804,7 +2690,7 @@ int mcpt_render_frames(mcpt_ctx *ctx, const mcpt_scene *scene, const mcpt_camera
         if (p->stripe_count > 1) HIP_OK(hipMemsetAsync(ctx->d_prim_cost, 0, (size_t)n_px * sizeof(uint32_t), st));
         if (scene->near4_bytes <= kPrimSmallTree) {
           // small trees: one ray per lane, one 8x8 tile per workgroup
-          const size_t lds_p = (size_t)(noprune ? scene->stack_depth : scene->stack_depth4) * 64 * sizeof(int32_t);
+          const size_t lds_p = (size_t)depth_entries * 64 * sizeof(int32_t);
           const dim3 g((unsigned)tiles);
           if (noprune)
             hipLaunchKernelGGL(k_primary<MCPT_MODE_NOPRUNE>, g, dim3(64), lds_p, st, A, ctx->d_prim);
@@ -2912,7 +2798,6 @@ int mcpt_render_frames(mcpt_ctx *ctx, const mcpt_scene *scene, const mcpt_camera
   ctx->last.frames_per_block = fpl_head;
   ctx->last.stack_window = win ? 1 : 0;
   ctx->last.quantized = kind == 2 ? 1 : 0;
-  ctx->last.wide_nodes = kind == 3 ? 1 : 0;
   ctx->last.workgroups = (int32_t)grid;
   ctx->last.primary_cache = prim_state;
   ctx->last_pending = true;

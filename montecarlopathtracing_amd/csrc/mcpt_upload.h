@@ -17,7 +17,6 @@ struct DeviceScene {
   int64_t n_near4, n_nodes4, n_int;
   int32_t stack_depth;  // the reference tree's DFS stack bound (mcpt_bvh_stack_depth)
   int32_t depth4;       // max of both 4-wide trees' stack needs
-  int32_t depth_ref4;   // the reference tree's 4-wide stack need alone (the 8-wide search's fallback)
   bool quant;           // near4q / triq built
   mcpt_bvh_node root;   // host copy of node 0
 };

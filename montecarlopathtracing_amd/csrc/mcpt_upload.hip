@@ -1051,7 +1051,6 @@ int build_scene_device(const mcpt_triangle *tris, int64_t n, const mcpt_bvh_node
   if (n == 1) {  // a single leaf: no nodes (mcpt_scene_upload keeps one zeroed record of each)
     out->stack_depth = 1;
     out->depth4 = 1;
-    out->depth_ref4 = 1;
     out->n_near4 = out->n_nodes4 = 1;
     UP_OK(hipMalloc(&out->nodes, sizeof(UDevNode)));
     UP_OK(hipMalloc(&out->nodes4, sizeof(Node4Rec)));
@@ -1136,7 +1135,6 @@ int build_scene_device(const mcpt_triangle *tris, int64_t n, const mcpt_bvh_node
     int32_t need0 = 0;
     if (int rc = d2h(&need0, need, 1, st)) return rc;
     out->depth4 = std::max(need0, 1);
-    out->depth_ref4 = out->depth4;
   }
 
   // ---- the SAH search tree over the reference's leaves

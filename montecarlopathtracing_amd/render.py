@@ -45,7 +45,7 @@ class DeviceScene:
     mats) whose tris / nodes are device byte tensors (mcpt_scene_upload_device:
     everything built on the GPU, the same bytes)."""
 
-    ARRAYS = ("near4", "near4q", "nodes4", "nodes", "tris", "triq", "meta", "near8")
+    ARRAYS = ("near4", "near4q", "nodes4", "nodes", "tris", "triq")
 
     def __init__(self, renderer, data):
         self.renderer = renderer

@@ -1,8 +1,7 @@
 // ref_runner.hip — TEST INFRASTRUCTURE ONLY (never linked into the product).
 //
 // Runs the reference's own OpenCL kernels — MonteCarloPathTracing/kernels/
-// {rayGenerator,intersect,shade,history,EPO}.cl with objdef.h prepended (and
-// testkernel.cl, ColorOut's display pass, without it, as colorout.cpp:32 builds it), compiled
+// {rayGenerator,intersect,shade,history,EPO}.cl with objdef.h prepended, compiled
 // UNMODIFIED for gfx950 by ROCm's OpenCL C compiler (oracle/Makefile, default
 // OpenCL build options exactly as OpenCLBasic::createProgramFromFileWithHeader
 // passes them, MCPT/oclbasic.cpp:167-183) — on the GPU through the HIP module
@@ -314,46 +313,6 @@ int ref_rcp_f32(const float *in, float *out, int64_t n) {
   CK(hipDeviceSynchronize());
   TRY(d.down(out));
   return 0;
-}
-
-// testkernel.cl func (ColorOut's display pass, colorout.cpp:32-33,58-70):
-// the unmodified kernel writes the RGBA32F image the reference shares with
-// GL.  Its image2d_t argument is, in the AMDGPU kernel ABI, a constant-
-// address pointer to the image's resource descriptor, which is what a HIP
-// surface object is (ROCclr builds both; hip/amd_detail/amd_surface_functions.h
-// passes it to the same __ockl_image_store_2D that write_imagef lowers to).
-// So the kernel runs headless on a float4 hipArray bound as a surface, and the
-// image is copied back row by row (NDRange {W, H}).
-int ref_gamma_preview(const float *color, int32_t w, int32_t h, float *out) {
-  hipFunction_t f;
-  TRY(get_fn("testkernel.co", "func", &f));
-  Dev<float> dc;
-  TRY(dc.alloc((size_t)w * h * 4));
-  TRY(dc.up(color));
-  hipArray_t arr = nullptr;
-  hipChannelFormatDesc fmt = hipCreateChannelDesc(32, 32, 32, 32, hipChannelFormatKindFloat);
-  CK(hipMallocArray(&arr, &fmt, (size_t)w, (size_t)h, hipArraySurfaceLoadStore));
-  hipResourceDesc rd;
-  std::memset(&rd, 0, sizeof(rd));
-  rd.resType = hipResourceTypeArray;
-  rd.res.array.array = arr;
-  hipSurfaceObject_t surf = nullptr;
-  hipError_t e = hipCreateSurfaceObject(&surf, &rd);
-  if (e != hipSuccess) {
-    (void)hipFreeArray(arr);
-    return err(std::string("hipCreateSurfaceObject: ") + hipGetErrorString(e));
-  }
-  void *args[] = {&surf, &dc.p};
-  int rc = launch2d(f, (uint32_t)w, (uint32_t)h, args);
-  if (rc == 0) {
-    e = hipDeviceSynchronize();
-    if (e == hipSuccess)
-      e = hipMemcpy2DFromArray(out, (size_t)w * 16, arr, 0, 0, (size_t)w * 16, (size_t)h, hipMemcpyDeviceToHost);
-    if (e != hipSuccess) rc = err(std::string("testkernel: ") + hipGetErrorString(e));
-  }
-  (void)hipDestroySurfaceObject(surf);
-  (void)hipFreeArray(arr);
-  return rc;
 }
 
 }  // extern "C"

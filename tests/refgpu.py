@@ -26,7 +26,7 @@ def so():
         s = ctypes.CDLL(os.path.join(REF_DIR, "libref_runner.so"))
         s.ref_last_error.restype = ctypes.c_char_p
         for n in ("ref_init", "ref_generate", "ref_intersect", "ref_shade", "ref_accumulate", "ref_render", "ref_epo",
-                  "ref_rcp_f32", "ref_gamma_preview"):
+                  "ref_rcp_f32"):
             getattr(s, n).restype = ctypes.c_int
         if s.ref_init(REF_DIR.encode()) != 0:
             raise RuntimeError(s.ref_last_error().decode())
@@ -100,11 +100,3 @@ def rcp_f32(x):
     _ck(so().ref_rcp_f32(P(a), P(out), i64(len(a))))
     return out
 
-
-def gamma_preview(colors, w, h):
-    """testkernel.cl func (ColorOut's display pass, the reference's own code
-    object) on a W x H float4 image: its RGBA32F output image, row-major."""
-    c = np.ascontiguousarray(colors, np.float32).reshape(h * w, 4)
-    out = np.zeros((h * w, 4), np.float32)
-    _ck(so().ref_gamma_preview(P(c), i32(w), i32(h), P(out)))
-    return out

@@ -27,7 +27,7 @@ from .test_gpu_parity import _render_both, assert_bits_equal, needs_ref  # noqa:
 # (scene, camera, width, height, depth, frames, MAX_ATTEMPT): C1 is config.json's
 # configid 2 at its own size; C3 is veach_mis at C3's size and depth, 4 frames
 CASES = {"C1": (scenes.cbox, scenes.CBOX_CAM, 256, 256, 4, 16, 16),
-         "C3": (scenes.mis, scenes.MIS_CAM, 1024, 1024, 12, 4, 1 << 20)}
+         "C3": (scenes.mis, scenes.MIS_CAM, 1024, 1024, 12, 4, 1 << 30)}
 
 
 @pytest.fixture(scope="module")

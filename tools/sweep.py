@@ -135,7 +135,6 @@ def main():
                         "waiting_frac": round(c["lane_waiting"] / (64.0 * max(c["wave_iterations"], 1)), 4),
                         "idle_frac": round(c["lane_idle"] / (64.0 * max(c["wave_iterations"], 1)), 4),
                         "iters_per_seg": round(c["wave_iterations"] * 64.0 / seg, 3),
-                        "helped_frac": round(c.get("helped_steps", 0) / max(c["node_visits"], 1), 4),
                         "order_fallbacks": c["order_fallbacks"]})
         print(json.dumps(rec), flush=True)
         out.append(rec)

@@ -3,7 +3,7 @@
 // node's other passing slots are pushed (design aid for DESIGN.md §3.3; not
 // a parity tool: the triangle test is plain Moller-Trumbore, the bounce a
 // cosine-free uniform hemisphere draw).
-//   g++ -O2 -std=c++17 -pthread -I montecarlopathtracing_amd/csrc tools/wide_order_sim.cpp \
+//   g++ -O2 -std=c++17 -pthread -I montecarlopathtracing_amd/csrc -I tools tools/wide_order_sim.cpp \
 //       montecarlopathtracing_amd/csrc/mcpt_host.cpp montecarlopathtracing_amd/csrc/mcpt_sah.cpp -o /tmp/wos
 //   /tmp/wos scenes/cbox/ cbox.obj 278 273 -800  278 273 -799  39.3077  [rays]
 #include <algorithm>
@@ -16,6 +16,7 @@
 
 #include "../include/mcpt_hip.h"
 #include "mcpt_bvh4.h"
+#include "wide8.h"
 
 namespace {
 struct V {
@@ -131,10 +132,10 @@ int main(int argc, char **argv) {
       L.push_back(r);
     }
   std::vector<mcpt::Node4Rec> t4;
-  std::vector<mcpt::Node8Rec> t8;
+  std::vector<mcpt::wide8::Node8Rec> t8;
   int32_t need4, need8;
   mcpt::build_sah4(L, t4, &need4, 8);
-  mcpt::widen_sah8(t4, t8, &need8);
+  mcpt::wide8::widen_sah8(t4, t8, &need8);
   const mcpt_bvh_node &root = B[0];
   float dx = root.bbmax[0] - root.bbmin[0], dy = root.bbmax[1] - root.bbmin[1], dz = root.bbmax[2] - root.bbmin[2];
   const float margin = std::ldexp(std::sqrt(dx * dx + dy * dy + dz * dz), -10);
@@ -144,7 +145,7 @@ int main(int argc, char **argv) {
   const int rays = argc > 10 ? atoi(argv[10]) : 20000;
   V fw = norm(sub(at, eye)), rt = norm(cross(fw, V{0, 1, 0})), up = cross(rt, fw);
   Search<4, mcpt::Node4Rec> s4{t4, T, 0};
-  Search<8, mcpt::Node8Rec> s8a{t8, T, 0}, s8b{t8, T, 1};
+  Search<8, mcpt::wide8::Node8Rec> s8a{t8, T, 0}, s8b{t8, T, 1};
   Search<4, mcpt::Node4Rec> s4b{t4, T, 1};
   std::mt19937 g(1);
   std::uniform_real_distribution<float> u01(0.0f, 1.0f);
