@@ -176,6 +176,8 @@ typedef struct mcpt_stats {
                                        primary hits; 2: it computed them too  */
   double   primary_ms;              /* primary_cache 2: device time of the
                                        primary-hit pass (part of kernel_ms)   */
+  int32_t  top_levels;              /* the search tree's top levels the last
+                                       call kept in LDS (mcpt_tuning.top_levels) */
 } mcpt_stats;
 
 /* Launch-plan knobs of the fused kernel (speed only: every setting gives the
@@ -234,6 +236,11 @@ typedef struct mcpt_tuning {
                                consecutive slots are one 8x8 tile), 2 spread
                                (they are one pixel of each of 64 tiles, so one
                                tile's dear pixels run in different waves)      */
+  int32_t top_levels;       /* EXACT: the search tree's top levels kept in LDS,
+                               where a segment descends through them as it
+                               begins instead of one T-phase gather per level:
+                               0 auto (2; 3 on trees over 4 MiB), 1-3 levels,
+                               -1 none                                           */
 } mcpt_tuning;
 
 /* ------------------------------------------------------- version / errors */
@@ -241,7 +248,8 @@ typedef struct mcpt_tuning {
  * passed across the boundary changes size or layout, or an entry point its
  * arguments (3: mcpt_tuning's tile_order / pixel_spread,
  * mcpt_set_pixel_segments' capacity; 4: the rejected T-phase-helper and
- * merged-gather knobs and counters removed from mcpt_tuning / mcpt_stats).
+ * merged-gather knobs and counters removed from mcpt_tuning / mcpt_stats,
+ * `top_levels` added to both).
  * A binding checks mcpt_abi_version() == MCPT_ABI_VERSION once at load and
  * refuses a library built from another header.                           */
 #define MCPT_ABI_VERSION 4

@@ -51,14 +51,15 @@ class Stats(ctypes.Structure):
                 ("stack_window", ctypes.c_int32), ("workgroups", ctypes.c_int32),
                 ("debug_violations", ctypes.c_uint64), ("phase_ticks", ctypes.c_uint64 * 4),
                 ("leaf_rejects", ctypes.c_uint64), ("quantized", ctypes.c_int32), ("primary_cache", ctypes.c_int32),
-                ("primary_ms", ctypes.c_double)]
+                ("primary_ms", ctypes.c_double), ("top_levels", ctypes.c_int32)]
 
 
 class Tuning(ctypes.Structure):
     """mcpt_tuning: launch-plan knobs of k_render (speed only; 0 = default)."""
     _fields_ = [(n, ctypes.c_int32) for n in (
         "leaf_threshold", "shade_threshold", "queue_chunk", "block_entries", "max_block_frames", "stack_window",
-        "lds_pad", "queues", "fetch_threshold", "quantized", "primary_cache", "last_block_frames", "tile_order", "pixel_spread")]
+        "lds_pad", "queues", "fetch_threshold", "quantized", "primary_cache", "last_block_frames", "tile_order", "pixel_spread",
+        "top_levels")]
 
 
 class MCPTError(RuntimeError):

@@ -41,7 +41,7 @@ using namespace mcpt;
 #define MCPT_WAVES_PER_SIMD 4  // k_render occupancy target (tools/sweep.py over `make variants`)
 #endif
 #ifndef MCPT_STACK_WINDOW_K
-#define MCPT_STACK_WINDOW_K 32
+#define MCPT_STACK_WINDOW_K 16  // 16: room in LDS for the tree's top levels (C2 / C4 even with 32; C3 -1 %)
 #endif
 constexpr int kStackWindow = MCPT_STACK_WINDOW_K;  // k_render's LDS window when the whole stack would cost occupancy
 
@@ -783,7 +783,16 @@ __device__ inline void handoff_store2(__amdgpu_buffer_rsrc_t rs, uint32_t off, u
 // 88 dequeues/us; sharded per XCD the rate scales with the heads).
 __device__ inline uint32_t xcc_id() { return __builtin_amdgcn_s_getreg((3 << 11) | 20) & 7u; }  // hwreg(HW_REG_XCC_ID, 0, 4)
 
-// Uniforms of a launch kept in LDS (k_render).  80-B camera + 16 + 32 B.
+// The search tree's top levels in LDS (RenderArgs::top_levels, 0-3;
+// mcpt_tuning.top_levels): a complete 4-ary layout after the uniforms, node i's
+// slot-k child at 4i + 1 + k, 112 B each (six plane quads and the links).  A
+// segment descends through them where it begins (the S phase) instead of
+// taking one T-phase gather per level: every traced segment starts at the
+// root and enters one node per level.
+constexpr int kMaxTopLevels = 3;
+__host__ __device__ constexpr int top_nodes(int levels) { return levels <= 0 ? 0 : (levels == 1 ? 1 : (levels == 2 ? 5 : 21)); }
+
+// Uniforms of a launch kept in LDS (k_render).  80-B camera + 16 + 32 + 16 B.
 struct __attribute__((aligned(16))) LdsUniforms {
   mcpt_camera cam;
   f4 cc;  // generateRay's 0.5 / tan(arg / 2) and W / H (cam_const)
@@ -811,6 +820,7 @@ struct RenderArgs {
   uint32_t *queue;            // n_queues work-queue heads, kQueueStride apart (zeroed before each launch)
   uint32_t n_queues;          // 1..kQueues
   int32_t lds_mats;           // 1: copy the material table to LDS after the stack
+  int32_t top_levels;         // EXACT: the search tree's top levels kept in LDS (0-3)
   int32_t chunk;              // queue entries a wave claims per atomic (at least)
   int32_t th_fetch;           // lanes needing an entry before the wave claims
   int32_t *spill;             // WindowStack spill areas, one per resident lane
@@ -895,10 +905,26 @@ __global__ void __launch_bounds__(64, MCPT_WAVES_PER_SIMD) k_render(RenderArgs A
     gen_ray_px(A.cam, c0, 0u, 0u, (uint32_t)A.W, (uint32_t)A.H, o0, d0);
     U->ray_u = A.cam.camera_type == 0 ? o0 : d0;
   }
+  // the top nodes follow the uniforms, the material table follows them
+  f4 *const top4 = reinterpret_cast<f4 *>(U + 1);
+  const int n_top = LIT || S.root_leaf >= 0 ? 0 : top_nodes(A.top_levels);
+  if (n_top > 0) {
+    // the top levels (the 128-B tree's; the quantized tree has the same ids and
+    // links): lane-strided over the nodes' 16-B quads, node by node in layout
+    // order; a slot's child id comes from its parent's links in global memory
+    for (int e = lane; e < n_top * 7; e += 64) {
+      const int i = e / 7, w = e % 7;
+      int lv[3], nl = 0;  // the slots on the path from the root, deepest first
+      for (int up = i; up > 0; up = (up - 1) >> 2) lv[nl++] = (up - 1) & 3;
+      int32_t id = 0;  // layout node i's id, or < 0 (a leaf or an empty slot on the path)
+      for (int t = nl - 1; t >= 0 && id >= 0; --t) id = S.near4[id].link[lv[t]];
+      if (id >= 0) top4[i * 7 + w] = reinterpret_cast<const f4 *>(S.near4 + id)[w];
+    }
+  }
   typedef const __attribute__((address_space(3))) mcpt_material LdsMaterial;
-  LdsMaterial *const lds_mat_table = (LdsMaterial *)reinterpret_cast<mcpt_material *>(U + 1);
+  LdsMaterial *const lds_mat_table = (LdsMaterial *)reinterpret_cast<mcpt_material *>(top4 + n_top * 7);
   if (A.lds_mats) {
-    mcpt_material *lm = reinterpret_cast<mcpt_material *>(U + 1);
+    mcpt_material *lm = reinterpret_cast<mcpt_material *>(top4 + n_top * 7);
     for (int k = lane; k < S.n_mats; k += 64) lm[k] = S.mats[k];
   }
   __syncthreads();
@@ -944,10 +970,36 @@ __global__ void __launch_bounds__(64, MCPT_WAVES_PER_SIMD) k_render(RenderArgs A
     t2 = kFltMax;
     ref = LIT;
     sp = 0;
-    if (slab_pass(box_test<LIT>(U->root_min.xyz, U->root_max.xyz, o.xyz, d.xyz, rinv), kTmin))
-      cur = S.root_leaf >= 0 ? ~S.root_leaf : 0;
-    else
+    if (!slab_pass(box_test<LIT>(U->root_min.xyz, U->root_max.xyz, o.xyz, d.xyz, rinv), kTmin)) {
       cur = kDone;
+    } else if (S.root_leaf >= 0) {
+      cur = ~S.root_leaf;
+    } else if (!LIT && n_top > 0) {
+      // the top levels from LDS (ds_read_b128; at the root the same address in
+      // every lane): the exact 128-B nodes also for the quantized tree, whose
+      // node ids and links are the 128-B tree's -- exact boxes are the
+      // union-of-leaf boxes the candidate-set argument needs
+      typedef const __attribute__((address_space(3))) f4 LdsF4;
+      uint32_t ctr = 0;
+      int ti = 0;  // layout index of the node to step
+      cur = 0;
+#pragma unroll
+      for (int lvl = 0; lvl < kMaxTopLevels; ++lvl) {
+        if (lvl >= A.top_levels) break;
+        LdsF4 *rq = (LdsF4 *)(top4 + ti * 7);
+        const f4 q0 = rq[0], q1 = rq[1], q2 = rq[2], q3 = rq[3], q4 = rq[4], q5 = rq[5], lk = rq[6];
+        cur = step4q<PRUNE>(q0, q1, q2, q3, q4, q5, as_i(lk.x), as_i(lk.y), as_i(lk.z), as_i(lk.w), o.xyz, rinv, kTmin,
+                            best_t + S.prune_margin, true, sk, sp, ctr);
+        // the entered slot's child, when it is internal: the next level's node
+        const int k = cur < 0 ? -1 : (cur == as_i(lk.x) ? 0 : (cur == as_i(lk.y) ? 1 : (cur == as_i(lk.z) ? 2 : 3)));
+        ti = k < 0 ? -1 : 4 * ti + 1 + k;
+        if (ti < 0) break;
+      }
+      if (STATS) n_nodes += ctr;
+      if (cur == kPop) cur = pop_next();
+    } else {
+      cur = 0;
+    }
   };
   // a frame's first segment: the primary ray and its hit are the same every
   // frame (the primary-hit pass computed them once), so the lane takes both
@@ -1924,7 +1976,7 @@ int mcpt_set_tuning(mcpt_ctx *c, const mcpt_tuning *t) {
             t->primary_cache < 0 || t->primary_cache > 2 || t->lds_pad < 0 || t->lds_pad > 65536 ||
             t->queue_chunk > 4096 || t->leaf_threshold > 64 || t->shade_threshold > 64 || t->fetch_threshold > 64 ||
             t->last_block_frames < -1 || t->tile_order < 0 || t->tile_order > 2 || t->pixel_spread < 0 ||
-            t->pixel_spread > 2))
+            t->pixel_spread > 2 || t->top_levels < -1 || t->top_levels > kMaxTopLevels))
     return mcpt::fail(MCPT_ERR_ARG, "set_tuning: value out of range");
   if (t)
     c->tune = *t;
@@ -2456,8 +2508,18 @@ int mcpt_render_frames(mcpt_ctx *ctx, const mcpt_scene *scene, const mcpt_camera
   const int kind = noprune ? 1 : (quant ? 2 : 0);
   const int glossy = scene->has_glossy ? 1 : 0;  // the shading instantiation (speed only: same bits)
   const size_t pad = (size_t)std::max(0, T.lds_pad);
-  const size_t lds_plain = (((size_t)depth_entries * 64 * sizeof(int32_t) + sizeof(LdsUniforms) + lds_mats + 15) & ~(size_t)15) + pad;
-  const size_t lds_win = (((size_t)kStackWindow * 64 * sizeof(int32_t) + sizeof(LdsUniforms) + lds_mats + 15) & ~(size_t)15) + pad;
+  // the search tree's top levels in LDS, stepped where a segment begins
+  // (EXACT; k_render): auto 2, 3 on trees over 4 MiB (DESIGN.md §3.4:
+  // against none, C2 -2.7 %, C3 -5.8 %, C4 -7.6 % with 2 and -12.4 % with 3,
+  // where C2 and C3 lose 3-5 % with 3)
+  A.top_levels = noprune || scene->view.root_leaf >= 0 ? 0
+               : (T.top_levels < 0 ? 0 : (T.top_levels > 0 ? std::min(T.top_levels, kMaxTopLevels)
+                                                              : (scene->near4_bytes > (4ll << 20) ? 3 : 2)));
+  const size_t lds_top = (size_t)top_nodes(A.top_levels) * 7 * sizeof(f4);
+  const size_t lds_plain =
+      (((size_t)depth_entries * 64 * sizeof(int32_t) + sizeof(LdsUniforms) + lds_top + lds_mats + 15) & ~(size_t)15) + pad;
+  const size_t lds_win =
+      (((size_t)kStackWindow * 64 * sizeof(int32_t) + sizeof(LdsUniforms) + lds_top + lds_mats + 15) & ~(size_t)15) + pad;
   bool win = false;
   int per_cu = 0;
   if (T.stack_window == 1) {  // forced (tests, experiments): the window even when the whole stack fits in it
@@ -2798,6 +2860,7 @@ int mcpt_render_frames(mcpt_ctx *ctx, const mcpt_scene *scene, const mcpt_camera
   ctx->last.frames_per_block = fpl_head;
   ctx->last.stack_window = win ? 1 : 0;
   ctx->last.quantized = kind == 2 ? 1 : 0;
+  ctx->last.top_levels = A.top_levels;
   ctx->last.workgroups = (int32_t)grid;
   ctx->last.primary_cache = prim_state;
   ctx->last_pending = true;
