@@ -776,3 +776,54 @@ def test_handoff_tag_wrap_bitexact(rnd):
         assert_bits_equal(b.hist.cpu().numpy(), rh, "hist vs reference")
         assert_bits_equal(b.seeds_np(), rs, "seeds vs reference")
     dsc.close()
+
+
+@needs_ref
+@pytest.mark.parametrize("name,getter,camjson,depth", [("cbox", scenes.cbox, scenes.CBOX_CAM, 6),
+                                                       ("mis", scenes.mis, scenes.MIS_CAM, 12),
+                                                       ("dining", scenes.dining, scenes.DINING_CAM, 16)])
+@pytest.mark.parametrize("levels", [-1, 1, 2, 3])
+@pytest.mark.parametrize("quantized", [1, 2])
+def test_top_levels_bitexact(rnd, name, getter, camjson, depth, levels, quantized):
+    """The search tree's top levels in LDS (mcpt_tuning.top_levels: none, 1, 2
+    or 3 levels descended where a segment begins, from the exact 128-B nodes
+    also for the quantized tree): every setting matches the reference kernels
+    bit for bit, with either node format."""
+    rnd.set_tuning(top_levels=levels, quantized=quantized)
+    try:
+        (h_, c_, s_), (rh, rc, rs) = _render_both(rnd, getter(), camjson, 64, 64, depth, 4, 4)
+        st = rnd.stats()
+    finally:
+        rnd.set_tuning()
+    assert st["top_levels"] == (0 if levels < 0 else levels) and st["quantized"] == (1 if quantized == 1 else 0)
+    assert_bits_equal(c_, rc, "count")
+    assert_bits_equal(s_, rs, "seeds")
+    assert_bits_equal(h_, rh, "hist")
+
+
+def test_top_levels_full_size_same_bits(rnd):
+    """Size-independent property at C2's and C4's sizes: every top_levels
+    setting gives the same image, on the whole image and on an 8-rank share;
+    auto takes 2 levels on cbox (2.1 MB tree) and 3 on the dining proxy."""
+    for getter, camjson, depth, w, h, frames, auto in ((scenes.cbox_diffuse, scenes.CBOX_CAM, 8, 1024, 1024, 6, 2),
+                                                       (scenes.dining, scenes.DINING_CAM, 16, 1920, 1080, 2, 3)):
+        data, cam = getter(), S.parse_camera(camjson)
+        seeds = R.default_seeds(w * h)
+        dsc = rnd.upload(data)
+        try:
+            for stripes in (1, 8):
+                outs = []
+                for levels in (-1, 0, 3):
+                    rnd.set_tuning(top_levels=levels)
+                    st = rnd.new_state(w, h, seeds)
+                    rnd.render_frames(dsc, cam, st, depth, 1 << 30, frames, stripe_rows=16, stripe_index=stripes - 1,
+                                      stripe_count=stripes)
+                    torch.cuda.synchronize()
+                    assert rnd.stats()["top_levels"] == {-1: 0, 0: auto, 3: 3}[levels]
+                    outs.append((st.hist.cpu().numpy(), st.count.cpu().numpy(), st.seeds_np()))
+                for o in outs[1:]:
+                    for a, b, what in zip(outs[0], o, ("hist", "count", "seeds")):
+                        assert_bits_equal(a, b, "%s / %d stripes" % (what, stripes))
+        finally:
+            rnd.set_tuning()
+            dsc.close()
