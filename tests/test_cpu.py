@@ -850,7 +850,7 @@ def test_variant_names_map_to_macros(tmp_path):
     assert len(lines) == 2
     macros = [dict(re.findall(r"-D(MCPT_[A-Z_]+)=(\S+)", ln)) for ln in lines]
     assert macros[0] == {"MCPT_WAVES_PER_SIMD": "4", "MCPT_STACK_WINDOW_K": "16", "MCPT_POW_LOBE": "1"}
-    assert macros[1] == {"MCPT_WAVES_PER_SIMD": "5", "MCPT_STACK_WINDOW_K": "32", "MCPT_POW_LOBE": "0"}
+    assert macros[1] == {"MCPT_WAVES_PER_SIMD": "5", "MCPT_STACK_WINDOW_K": "16", "MCPT_POW_LOBE": "0"}
 
 
 def test_bench_refuses_more_ranks_than_gpus():
