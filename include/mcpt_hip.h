@@ -239,7 +239,7 @@ typedef struct mcpt_tuning {
   int32_t top_levels;       /* EXACT: the search tree's top levels kept in LDS,
                                where a segment descends through them as it
                                begins instead of one T-phase gather per level:
-                               0 auto (2; 3 on trees over 4 MiB), 1-3 levels,
+                               0 auto (2; 4 on trees over 4 MiB), 1-4 levels,
                                -1 none                                           */
 } mcpt_tuning;
 

@@ -783,14 +783,26 @@ __device__ inline void handoff_store2(__amdgpu_buffer_rsrc_t rs, uint32_t off, u
 // 88 dequeues/us; sharded per XCD the rate scales with the heads).
 __device__ inline uint32_t xcc_id() { return __builtin_amdgcn_s_getreg((3 << 11) | 20) & 7u; }  // hwreg(HW_REG_XCC_ID, 0, 4)
 
-// The search tree's top levels in LDS (RenderArgs::top_levels, 0-3;
+// The search tree's top levels in LDS (RenderArgs::top_levels, 0-kMaxTopLevels;
 // mcpt_tuning.top_levels): a complete 4-ary layout after the uniforms, node i's
 // slot-k child at 4i + 1 + k, 112 B each (six plane quads and the links).  A
 // segment descends through them where it begins (the S phase) instead of
 // taking one T-phase gather per level: every traced segment starts at the
 // root and enters one node per level.
-constexpr int kMaxTopLevels = 3;
-__host__ __device__ constexpr int top_nodes(int levels) { return levels <= 0 ? 0 : (levels == 1 ? 1 : (levels == 2 ? 5 : 21)); }
+// MCPT_WG_WAVES: waves per k_render workgroup (4 shipped).  A workgroup's
+// waves share one copy of the uniforms, the top levels and the materials (each
+// wave keeps its own stack), so the LDS per wave shrinks and a fourth level
+// (85 nodes, 9.3 KB) fits.  Against one wave per workgroup: C3 -5.0 %, C4
+// -2.2 % at 3 levels and -7.0 % at 4, C2 and C5 even (profiles/r06_wg_waves.jsonl).
+#ifndef MCPT_WG_WAVES
+#define MCPT_WG_WAVES 4
+#endif
+constexpr int kWgWaves = MCPT_WG_WAVES;
+static_assert(kWgWaves == 1 || kWgWaves == 2 || kWgWaves == 4, "k_render workgroups of 1, 2 or 4 waves");
+constexpr int kMaxTopLevels = kWgWaves > 1 ? 4 : 3;
+__host__ __device__ constexpr int top_nodes(int levels) {
+  return levels <= 0 ? 0 : (levels == 1 ? 1 : (levels == 2 ? 5 : (levels == 3 ? 21 : 85)));
+}
 
 // Uniforms of a launch kept in LDS (k_render).  80-B camera + 16 + 32 + 16 B.
 struct __attribute__((aligned(16))) LdsUniforms {
@@ -820,7 +832,7 @@ struct RenderArgs {
   uint32_t *queue;            // n_queues work-queue heads, kQueueStride apart (zeroed before each launch)
   uint32_t n_queues;          // 1..kQueues
   int32_t lds_mats;           // 1: copy the material table to LDS after the stack
-  int32_t top_levels;         // EXACT: the search tree's top levels kept in LDS (0-3)
+  int32_t top_levels;         // EXACT: the search tree's top levels kept in LDS (0-kMaxTopLevels)
   int32_t chunk;              // queue entries a wave claims per atomic (at least)
   int32_t th_fetch;           // lanes needing an entry before the wave claims
   int32_t *spill;             // WindowStack spill areas, one per resident lane
@@ -873,20 +885,24 @@ __device__ inline uint32_t queue_items(uint32_t x, uint32_t n_tiles, uint32_t nq
 // no pixel state; a lane traces its pixel's primary ray, stores the closest
 // hit at the S phase instead of shading, and takes the next pixel.
 template <int MODE, bool STATS, bool WIN, bool PAIR, bool Q, bool PRIM = false, bool G = true>
-__global__ void __launch_bounds__(64, MCPT_WAVES_PER_SIMD) k_render(RenderArgs A) {
+__global__ void __launch_bounds__(64 * kWgWaves, MCPT_WAVES_PER_SIMD) k_render(RenderArgs A) {
   constexpr bool PRUNE = MODE != MCPT_MODE_NOPRUNE;
   constexpr bool LIT = MODE == MCPT_MODE_NOPRUNE;
   static_assert(!(Q && LIT), "the quantized search tree is an EXACT-mode structure");
   extern __shared__ int32_t lds_stack[];
-  const int lane = threadIdx.x;
+  const int lane = threadIdx.x & 63;
+  const int wv = kWgWaves > 1 ? (int)(threadIdx.x >> 6) : 0;  // this wave in its workgroup
+  const size_t gwave = (size_t)blockIdx.x * kWgWaves + wv;      // this wave in the launch
   // the whole stack in LDS, or its top kStackWindow entries (deep trees, where
-  // the whole stack would cap the resident waves per CU; chosen at launch)
+  // the whole stack would cap the resident waves per CU; chosen at launch);
+  // each wave of the workgroup has its own
   using Stack = typename std::conditional<WIN, WindowStack<kStackWindow>, PlainStack>::type;
   Stack stk;
+  int32_t *const my_stack = lds_stack + (size_t)wv * A.stack_depth * 64;
   if constexpr (WIN)
-    stk = Stack{lds_stack + lane, A.spill + ((size_t)blockIdx.x * 64 + lane) * (size_t)A.spill_stride};
+    stk = Stack{my_stack + lane, A.spill + (gwave * 64 + lane) * (size_t)A.spill_stride};
   else
-    stk = Stack{lds_stack + lane, 64};
+    stk = Stack{my_stack + lane, 64};
   const SceneView &S = A.S;
   const int stack_cap = WIN ? kStackWindow + A.spill_stride : A.stack_depth;  // entries (MCPT_DEBUG bound)
   (void)stack_cap;
@@ -894,8 +910,8 @@ __global__ void __launch_bounds__(64, MCPT_WAVES_PER_SIMD) k_render(RenderArgs A
   // starts read (camera, generateRay constants, root box: kept out of the
   // SGPRs, the scarce register file of this kernel), then the material table
   // (small tables only)
-  LdsUniforms *U = reinterpret_cast<LdsUniforms *>(lds_stack + A.stack_depth * 64);
-  if (lane == 0) {
+  LdsUniforms *U = reinterpret_cast<LdsUniforms *>(lds_stack + (size_t)kWgWaves * A.stack_depth * 64);
+  if (threadIdx.x == 0) {
     U->cam = A.cam;
     const CamConst c0 = cam_const(A.cam, (uint32_t)A.W, (uint32_t)A.H);
     U->cc = (f4){c0.distance, c0.ratio, 0.0f, 0.0f};
@@ -912,9 +928,9 @@ __global__ void __launch_bounds__(64, MCPT_WAVES_PER_SIMD) k_render(RenderArgs A
     // the top levels (the 128-B tree's; the quantized tree has the same ids and
     // links): lane-strided over the nodes' 16-B quads, node by node in layout
     // order; a slot's child id comes from its parent's links in global memory
-    for (int e = lane; e < n_top * 7; e += 64) {
+    for (int e = (int)threadIdx.x; e < n_top * 7; e += 64 * kWgWaves) {
       const int i = e / 7, w = e % 7;
-      int lv[3], nl = 0;  // the slots on the path from the root, deepest first
+      int lv[4], nl = 0;  // the slots on the path from the root, deepest first
       for (int up = i; up > 0; up = (up - 1) >> 2) lv[nl++] = (up - 1) & 3;
       int32_t id = 0;  // layout node i's id, or < 0 (a leaf or an empty slot on the path)
       for (int t = nl - 1; t >= 0 && id >= 0; --t) id = S.near4[id].link[lv[t]];
@@ -925,7 +941,7 @@ __global__ void __launch_bounds__(64, MCPT_WAVES_PER_SIMD) k_render(RenderArgs A
   LdsMaterial *const lds_mat_table = (LdsMaterial *)reinterpret_cast<mcpt_material *>(top4 + n_top * 7);
   if (A.lds_mats) {
     mcpt_material *lm = reinterpret_cast<mcpt_material *>(top4 + n_top * 7);
-    for (int k = lane; k < S.n_mats; k += 64) lm[k] = S.mats[k];
+    for (int k = (int)threadIdx.x; k < S.n_mats; k += 64 * kWgWaves) lm[k] = S.mats[k];
   }
   __syncthreads();
 
@@ -944,7 +960,7 @@ __global__ void __launch_bounds__(64, MCPT_WAVES_PER_SIMD) k_render(RenderArgs A
   int32_t blk = 0;             // frame block of the pixel (the pending entry's block while kPend)
   f4 hist = (f4){0.0f, 0.0f, 0.0f, 0.0f};
   f4 o = hist, d = hist, color = hist;
-  auto primary = [&]() {  // no jitter: every frame re-shoots the same primary ray
+  auto primary = [&]() __attribute__((always_inline)) {  // no jitter: every frame re-shoots the same primary ray
     const f4 c4 = U->cc;
     CamConst cc;
     cc.distance = c4.x;
@@ -961,8 +977,8 @@ __global__ void __launch_bounds__(64, MCPT_WAVES_PER_SIMD) k_render(RenderArgs A
   bool ref = LIT;
   float t2 = kFltMax;
   const Stack &sk = stk;
-  auto pop_next = [&]() -> int32_t { return sp == 0 ? kDone : sk.pop(sp); };
-  auto begin_segment = [&]() {
+  auto pop_next = [&]() __attribute__((always_inline)) -> int32_t { return sp == 0 ? kDone : sk.pop(sp); };
+  auto begin_segment = [&]() __attribute__((always_inline)) {
     rinv.x = __builtin_amdgcn_rcpf(d.x);
     rinv.y = __builtin_amdgcn_rcpf(d.y);
     rinv.z = __builtin_amdgcn_rcpf(d.z);
@@ -1004,7 +1020,7 @@ __global__ void __launch_bounds__(64, MCPT_WAVES_PER_SIMD) k_render(RenderArgs A
   // a frame's first segment: the primary ray and its hit are the same every
   // frame (the primary-hit pass computed them once), so the lane takes both
   // from the pixel's record and goes straight to S
-  auto begin_frame = [&]() {
+  auto begin_frame = [&]() __attribute__((always_inline)) {
     color = (f4){1.0f, 1.0f, 1.0f, 1.0f};
     if (A.prim) {
       const uint32_t pid = (pxy >> 16) * (uint32_t)A.W + (pxy & 0xFFFFu);
@@ -1452,7 +1468,7 @@ __global__ void __launch_bounds__(64, MCPT_WAVES_PER_SIMD) k_render(RenderArgs A
     const uint64_t last = red(rt_last, 1), started = red(n_started, 2), pend = red(pend_it, 2);
     const uint64_t rt_end = __builtin_amdgcn_s_memrealtime();
     if (A.wave_log && lane == 0) {
-      unsigned long long *w = A.wave_log + (size_t)blockIdx.x * kWaveLogWords;
+      unsigned long long *w = A.wave_log + gwave * kWaveLogWords;
       w[0] = rt_start;
       w[1] = dry == ~0ull ? rt_end : dry;
       w[2] = rt_end;
@@ -2409,8 +2425,9 @@ int mcpt_scene_destroy(mcpt_scene *s) {
   return MCPT_OK;
 }
 
-// Resident 64-lane workgroups per CU of a k_render instantiation at an LDS
-// size, asked once per (kernel, size) and kept in the context.
+// Resident workgroups (kWgWaves waves each) per CU of a k_render
+// instantiation at an LDS size, asked once per (kernel, size) and kept in the
+// context.
 static int occupancy(mcpt_ctx *ctx, const void *fn, size_t lds, int *out) {
   for (const auto &e : ctx->occ)
     if (e.fn == fn && e.lds == lds) {
@@ -2418,7 +2435,7 @@ static int occupancy(mcpt_ctx *ctx, const void *fn, size_t lds, int *out) {
       return MCPT_OK;
     }
   int n = 0;
-  HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, fn, 64, lds));
+  HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, fn, 64 * kWgWaves, lds));
   ctx->occ.push_back({fn, lds, n});
   *out = n;
   return MCPT_OK;
@@ -2509,17 +2526,19 @@ int mcpt_render_frames(mcpt_ctx *ctx, const mcpt_scene *scene, const mcpt_camera
   const int glossy = scene->has_glossy ? 1 : 0;  // the shading instantiation (speed only: same bits)
   const size_t pad = (size_t)std::max(0, T.lds_pad);
   // the search tree's top levels in LDS, stepped where a segment begins
-  // (EXACT; k_render): auto 2, 3 on trees over 4 MiB (DESIGN.md §3.4:
-  // against none, C2 -2.7 %, C3 -5.8 %, C4 -7.6 % with 2 and -12.4 % with 3,
-  // where C2 and C3 lose 3-5 % with 3)
+  // (EXACT; k_render): auto 2, kMaxTopLevels (4) on trees over 4 MiB
+  // (against none, C2 -2.7 %, C3 -5.8 %, C4 -7.6 % with 2 and
+  // -12.4 % with 3, where C2 and C3 lose 3-5 % with 3; 4-wave workgroups: C4 a
+  // further -4.9 % with 4 against 3, C5 even)
   A.top_levels = noprune || scene->view.root_leaf >= 0 ? 0
                : (T.top_levels < 0 ? 0 : (T.top_levels > 0 ? std::min(T.top_levels, kMaxTopLevels)
-                                                              : (scene->near4_bytes > (4ll << 20) ? 3 : 2)));
+                                                              : (scene->near4_bytes > (4ll << 20) ? kMaxTopLevels : 2)));
   const size_t lds_top = (size_t)top_nodes(A.top_levels) * 7 * sizeof(f4);
-  const size_t lds_plain =
-      (((size_t)depth_entries * 64 * sizeof(int32_t) + sizeof(LdsUniforms) + lds_top + lds_mats + 15) & ~(size_t)15) + pad;
-  const size_t lds_win =
-      (((size_t)kStackWindow * 64 * sizeof(int32_t) + sizeof(LdsUniforms) + lds_top + lds_mats + 15) & ~(size_t)15) + pad;
+  // a stack per wave; one copy of the uniforms, top levels and materials per workgroup
+  const size_t lds_plain = (((size_t)kWgWaves * depth_entries * 64 * sizeof(int32_t) + sizeof(LdsUniforms) + lds_top +
+                             lds_mats + 15) & ~(size_t)15) + pad;
+  const size_t lds_win = (((size_t)kWgWaves * kStackWindow * 64 * sizeof(int32_t) + sizeof(LdsUniforms) + lds_top +
+                           lds_mats + 15) & ~(size_t)15) + pad;
   bool win = false;
   int per_cu = 0;
   if (T.stack_window == 1) {  // forced (tests, experiments): the window even when the whole stack fits in it
@@ -2542,7 +2561,10 @@ int mcpt_render_frames(mcpt_ctx *ctx, const mcpt_scene *scene, const mcpt_camera
   const void *kfn = kfns[kind][ctx->stats_on][win][pair][glossy];
   A.stack_depth = win ? kStackWindow : depth_entries;  // the uniforms and material table follow the stack in LDS
   A.spill_stride = win ? std::max(0, depth_entries - kStackWindow) : 0;
-  const int64_t grid = std::max<int64_t>(1, std::min<int64_t>(tiles, (int64_t)std::max(per_cu, 1) * ctx->n_cu));
+  // grid_wg workgroups of kWgWaves waves: `grid` waves (a tile per wave at most)
+  const int64_t grid_wg = std::max<int64_t>(
+      1, std::min<int64_t>((tiles + kWgWaves - 1) / kWgWaves, (int64_t)std::max(per_cu, 1) * ctx->n_cu));
+  const int64_t grid = grid_wg * kWgWaves;
   const int64_t spill_need = win ? grid * 64 * (int64_t)A.spill_stride : 0;
   if (win && spill_need > ctx->spill_cap) {
     if (ctx->d_spill) HIP_OK(hipFree(ctx->d_spill));
@@ -2574,7 +2596,8 @@ int mcpt_render_frames(mcpt_ctx *ctx, const mcpt_scene *scene, const mcpt_camera
   int fpl = p->frames_per_launch;
   bool tail_ok = false;  // auto plan with several entries per lane: a short last block may apply
   double slots_per_px = 0;  // pixels per resident lane (auto plans)
-  const double px_per_lane = (double)n_items / ((double)std::max(per_cu, 1) * ctx->n_cu * 64);  // vs resident lanes
+  const double px_per_lane =
+      (double)n_items / ((double)std::max(per_cu, 1) * ctx->n_cu * 64 * kWgWaves);  // vs resident lanes
   if (fpl <= 0) {
     const int frames = std::max(p->frames, 1);
     const double per_block = (double)n_items / (double)(grid * 64);  // entries per lane per block
@@ -2783,8 +2806,9 @@ int mcpt_render_frames(mcpt_ctx *ctx, const mcpt_scene *scene, const mcpt_camera
           int per_cu_p = 0;
           rc = occupancy(ctx, pfn, lds, &per_cu_p);
           if (rc) return rc;
-          const int64_t grid_p = std::max<int64_t>(1, std::min<int64_t>(tiles, (int64_t)std::max(per_cu_p, 1) * ctx->n_cu));
-          const int64_t spill_p = win ? grid_p * 64 * (int64_t)A.spill_stride : 0;
+          const int64_t grid_pwg = std::max<int64_t>(
+              1, std::min<int64_t>((tiles + kWgWaves - 1) / kWgWaves, (int64_t)std::max(per_cu_p, 1) * ctx->n_cu));
+          const int64_t spill_p = win ? grid_pwg * kWgWaves * 64 * (int64_t)A.spill_stride : 0;
           if (spill_p > ctx->spill_cap) {
             if (ctx->d_spill) HIP_OK(hipFree(ctx->d_spill));
             ctx->d_spill = nullptr;
@@ -2795,7 +2819,7 @@ int mcpt_render_frames(mcpt_ctx *ctx, const mcpt_scene *scene, const mcpt_camera
           }
           Ap.spill = ctx->d_spill;
           void *pargs[] = {&Ap};
-          HIP_OK(hipLaunchKernel(pfn, dim3((unsigned)grid_p), dim3(64), pargs, lds, st));
+          HIP_OK(hipLaunchKernel(pfn, dim3((unsigned)grid_pwg), dim3(64 * kWgWaves), pargs, lds, st));
         }
         HIP_OK(hipEventRecord(ctx->ev_prim, st));
         ctx->prim_key = key;
@@ -2849,7 +2873,7 @@ int mcpt_render_frames(mcpt_ctx *ctx, const mcpt_scene *scene, const mcpt_camera
       }
       A.tag_base = (ctx->launch_seq & 0xFFu) << 8;
       void *kargs[] = {&A};
-      HIP_OK(hipLaunchKernel(kfn, dim3((unsigned)grid), dim3(64), kargs, lds, st));
+      HIP_OK(hipLaunchKernel(kfn, dim3((unsigned)grid_wg), dim3(64 * kWgWaves), kargs, lds, st));
       ++launches;
     }
   }

@@ -844,13 +844,15 @@ def test_variant_names_map_to_macros(tmp_path):
     values (dry run: the compiler is `echo`)."""
     import subprocess
     out = subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "montecarlopathtracing_amd", "csrc"), "variants",
-                          "VARIANTS=w4k16 w5l0", "HIPCC=echo", "OUT=%s" % tmp_path],
+                          "VARIANTS=w4k16 w5l0 w5g1", "HIPCC=echo", "OUT=%s" % tmp_path],
                          capture_output=True, text=True, check=True).stdout
     lines = [ln for ln in out.splitlines() if "mcpt_device.hip" in ln]
-    assert len(lines) == 2
+    assert len(lines) == 3
     macros = [dict(re.findall(r"-D(MCPT_[A-Z_]+)=(\S+)", ln)) for ln in lines]
-    assert macros[0] == {"MCPT_WAVES_PER_SIMD": "4", "MCPT_STACK_WINDOW_K": "16", "MCPT_POW_LOBE": "1"}
-    assert macros[1] == {"MCPT_WAVES_PER_SIMD": "5", "MCPT_STACK_WINDOW_K": "16", "MCPT_POW_LOBE": "0"}
+    shipped = {"MCPT_STACK_WINDOW_K": "16", "MCPT_POW_LOBE": "1", "MCPT_WG_WAVES": "4"}
+    assert macros[0] == dict(shipped, MCPT_WAVES_PER_SIMD="4")
+    assert macros[1] == dict(shipped, MCPT_WAVES_PER_SIMD="5", MCPT_POW_LOBE="0")
+    assert macros[2] == dict(shipped, MCPT_WAVES_PER_SIMD="5", MCPT_WG_WAVES="1")
 
 
 def test_bench_refuses_more_ranks_than_gpus():

@@ -782,14 +782,19 @@ def test_handoff_tag_wrap_bitexact(rnd):
 @pytest.mark.parametrize("name,getter,camjson,depth", [("cbox", scenes.cbox, scenes.CBOX_CAM, 6),
                                                        ("mis", scenes.mis, scenes.MIS_CAM, 12),
                                                        ("dining", scenes.dining, scenes.DINING_CAM, 16)])
-@pytest.mark.parametrize("levels", [-1, 1, 2, 3])
+@pytest.mark.parametrize("levels", [-1, 1, 2, 3, 4])
 @pytest.mark.parametrize("quantized", [1, 2])
 def test_top_levels_bitexact(rnd, name, getter, camjson, depth, levels, quantized):
     """The search tree's top levels in LDS (mcpt_tuning.top_levels: none, 1, 2
-    or 3 levels descended where a segment begins, from the exact 128-B nodes
-    also for the quantized tree): every setting matches the reference kernels
+    3 or 4 levels descended where a segment begins, from the exact 128-B nodes
+    also for the quantized tree; 4 needs several waves per workgroup,
+    MCPT_WG_WAVES, as shipped): every setting matches the reference kernels
     bit for bit, with either node format."""
-    rnd.set_tuning(top_levels=levels, quantized=quantized)
+    try:
+        rnd.set_tuning(top_levels=levels, quantized=quantized)
+    except L.MCPTError:
+        assert levels == 4
+        pytest.skip("this build keeps at most 3 levels (one wave per workgroup)")
     try:
         (h_, c_, s_), (rh, rc, rs) = _render_both(rnd, getter(), camjson, 64, 64, depth, 4, 4)
         st = rnd.stats()
@@ -804,9 +809,9 @@ def test_top_levels_bitexact(rnd, name, getter, camjson, depth, levels, quantize
 def test_top_levels_full_size_same_bits(rnd):
     """Size-independent property at C2's and C4's sizes: every top_levels
     setting gives the same image, on the whole image and on an 8-rank share;
-    auto takes 2 levels on cbox (2.1 MB tree) and 3 on the dining proxy."""
+    auto takes 2 levels on cbox (2.1 MB tree) and 4 on the dining proxy."""
     for getter, camjson, depth, w, h, frames, auto in ((scenes.cbox_diffuse, scenes.CBOX_CAM, 8, 1024, 1024, 6, 2),
-                                                       (scenes.dining, scenes.DINING_CAM, 16, 1920, 1080, 2, 3)):
+                                                       (scenes.dining, scenes.DINING_CAM, 16, 1920, 1080, 2, 4)):
         data, cam = getter(), S.parse_camera(camjson)
         seeds = R.default_seeds(w * h)
         dsc = rnd.upload(data)
