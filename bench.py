@@ -640,7 +640,10 @@ def main():
                           "last_block_frames": rnd.get_tuning()["last_block_frames"],
                           "tile_order": {0: "dearest first (costliest pixel)", 1: "image", 2: "dearest first (summed)"}[
                               rnd.get_tuning()["tile_order"]],
-                          "search_tree_nodes": search_tree},
+                          "search_tree_nodes": search_tree,
+                          "search_tree_top_levels_in_lds": kst.get("top_levels"),
+                          "stack": "16-entry LDS window + HBM spill" if kst.get("stack_window") else "whole in LDS",
+                          "resident_waves": kst.get("workgroups")},
                "active_Msegments_per_s": round(segments * n / elapsed / 1e6, 2),
                "scene_build_gpu_s": None if build_s is None else round(build_s, 3),
                "traced_Msegments_per_s": round(traced * n / elapsed / 1e6, 2),

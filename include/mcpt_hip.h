@@ -160,7 +160,8 @@ typedef struct mcpt_stats {
   uint64_t lane_idle;               /* lane-iterations with no pixel (queue
                                        claim pending, or the launch's tail)  */
   int32_t  stack_window;            /* 1: the last call ran the LDS-window stack */
-  int32_t  workgroups;              /* 64-lane workgroups per launch (resident grid) */
+  int32_t  workgroups;              /* 64-lane waves per launch (the resident grid;
+                                       a k_render workgroup holds 4 of them)      */
   uint64_t debug_violations;        /* MCPT_DEBUG builds: stack-bound, node- and
                                        triangle-index violations k_render caught
                                        (always 0 in release builds)           */
@@ -415,7 +416,7 @@ int mcpt_set_pixel_segments(mcpt_ctx *ctx, uint32_t *counts_dev, uint32_t *iters
 int mcpt_get_primary_cost(mcpt_ctx *ctx, uint32_t *out, int64_t cap, int64_t *n);
 
 /* Diagnostics (MCPT_PHASE_TIMING builds, libmcpt_hip_timing.so): the
- * timeline of every workgroup of the last render call's last k_render
+ * timeline of every 64-lane wave of the last render call's last k_render
  * launch, 8 words each: start, the first moment one of its lanes found every
  * work queue dry, end, the latest start of a queue entry (s_memrealtime
  * ticks, 100 MHz, chip-wide clock), loop iterations, entries started,
