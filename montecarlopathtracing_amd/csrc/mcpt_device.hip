@@ -792,8 +792,9 @@ __device__ inline uint32_t xcc_id() { return __builtin_amdgcn_s_getreg((3 << 11)
 // MCPT_WG_WAVES: waves per k_render workgroup (4 shipped).  A workgroup's
 // waves share one copy of the uniforms, the top levels and the materials (each
 // wave keeps its own stack), so the LDS per wave shrinks and a fourth level
-// (85 nodes, 9.3 KB) fits.  Against one wave per workgroup: C3 -5.0 %, C4
-// -2.2 % at 3 levels and -7.0 % at 4, C2 and C5 even (profiles/r06_wg_waves.jsonl).
+// (85 nodes, 9.3 KB) fits.  Against one wave per workgroup, both at the
+// shipped 4 waves per SIMD: C4 -3.4 %, C5 -1.2 %, the 8-rank shares of C2 / C4
+// / C5 -4.3 / -2.5 / -2.7 %, C2 and C3 even (profiles/r06_wg_waves_w4.jsonl).
 #ifndef MCPT_WG_WAVES
 #define MCPT_WG_WAVES 4
 #endif
@@ -2529,7 +2530,7 @@ int mcpt_render_frames(mcpt_ctx *ctx, const mcpt_scene *scene, const mcpt_camera
   // (EXACT; k_render): auto 2, kMaxTopLevels (4) on trees over 4 MiB
   // (against none, C2 -2.7 %, C3 -5.8 %, C4 -7.6 % with 2 and
   // -12.4 % with 3, where C2 and C3 lose 3-5 % with 3; 4-wave workgroups: C4 a
-  // further -4.9 % with 4 against 3, C5 even)
+  // further -4.2 % with 4 against 3, C5 -0.6 %)
   A.top_levels = noprune || scene->view.root_leaf >= 0 ? 0
                : (T.top_levels < 0 ? 0 : (T.top_levels > 0 ? std::min(T.top_levels, kMaxTopLevels)
                                                               : (scene->near4_bytes > (4ll << 20) ? kMaxTopLevels : 2)));
