@@ -799,10 +799,10 @@ __device__ inline uint32_t xcc_id() { return __builtin_amdgcn_s_getreg((3 << 11)
 #define MCPT_WG_WAVES 4
 #endif
 constexpr int kWgWaves = MCPT_WG_WAVES;
-static_assert(kWgWaves == 1 || kWgWaves == 2 || kWgWaves == 4, "k_render workgroups of 1, 2 or 4 waves");
-constexpr int kMaxTopLevels = kWgWaves > 1 ? 4 : 3;
+static_assert(kWgWaves == 1 || kWgWaves == 2 || kWgWaves == 4 || kWgWaves == 8, "k_render workgroups of 1-8 waves");
+constexpr int kMaxTopLevels = kWgWaves >= 8 ? 5 : (kWgWaves > 1 ? 4 : 3);
 __host__ __device__ constexpr int top_nodes(int levels) {
-  return levels <= 0 ? 0 : (levels == 1 ? 1 : (levels == 2 ? 5 : (levels == 3 ? 21 : 85)));
+  return levels <= 0 ? 0 : (levels == 1 ? 1 : (levels == 2 ? 5 : (levels == 3 ? 21 : (levels == 4 ? 85 : 341))));
 }
 
 // Uniforms of a launch kept in LDS (k_render).  80-B camera + 16 + 32 + 16 B.
@@ -931,7 +931,7 @@ __global__ void __launch_bounds__(64 * kWgWaves, MCPT_WAVES_PER_SIMD) k_render(R
     // order; a slot's child id comes from its parent's links in global memory
     for (int e = (int)threadIdx.x; e < n_top * 7; e += 64 * kWgWaves) {
       const int i = e / 7, w = e % 7;
-      int lv[4], nl = 0;  // the slots on the path from the root, deepest first
+      int lv[kMaxTopLevels], nl = 0;  // the slots on the path from the root, deepest first
       for (int up = i; up > 0; up = (up - 1) >> 2) lv[nl++] = (up - 1) & 3;
       int32_t id = 0;  // layout node i's id, or < 0 (a leaf or an empty slot on the path)
       for (int t = nl - 1; t >= 0 && id >= 0; --t) id = S.near4[id].link[lv[t]];

@@ -782,7 +782,7 @@ def test_handoff_tag_wrap_bitexact(rnd):
 @pytest.mark.parametrize("name,getter,camjson,depth", [("cbox", scenes.cbox, scenes.CBOX_CAM, 6),
                                                        ("mis", scenes.mis, scenes.MIS_CAM, 12),
                                                        ("dining", scenes.dining, scenes.DINING_CAM, 16)])
-@pytest.mark.parametrize("levels", [-1, 1, 2, 3, 4])
+@pytest.mark.parametrize("levels", [-1, 1, 2, 3, 4, 5])
 @pytest.mark.parametrize("quantized", [1, 2])
 def test_top_levels_bitexact(rnd, name, getter, camjson, depth, levels, quantized):
     """The search tree's top levels in LDS (mcpt_tuning.top_levels: none, 1, 2
@@ -793,8 +793,8 @@ def test_top_levels_bitexact(rnd, name, getter, camjson, depth, levels, quantize
     try:
         rnd.set_tuning(top_levels=levels, quantized=quantized)
     except L.MCPTError:
-        assert levels == 4
-        pytest.skip("this build keeps at most 3 levels (one wave per workgroup)")
+        assert levels >= 4
+        pytest.skip("this build keeps fewer levels (MCPT_WG_WAVES: 1 wave 3, 2-4 waves 4, 8 waves 5)")
     try:
         (h_, c_, s_), (rh, rc, rs) = _render_both(rnd, getter(), camjson, 64, 64, depth, 4, 4)
         st = rnd.stats()
@@ -806,12 +806,27 @@ def test_top_levels_bitexact(rnd, name, getter, camjson, depth, levels, quantize
     assert_bits_equal(h_, rh, "hist")
 
 
+def _max_top_levels(rnd):
+    """The most top levels this build keeps (MCPT_WG_WAVES: 3, 4 or 5)."""
+    for k in (5, 4):
+        try:
+            rnd.set_tuning(top_levels=k)
+            return k
+        except L.MCPTError:
+            pass
+        finally:
+            rnd.set_tuning()
+    return 3
+
+
 def test_top_levels_full_size_same_bits(rnd):
     """Size-independent property at C2's and C4's sizes: every top_levels
     setting gives the same image, on the whole image and on an 8-rank share;
-    auto takes 2 levels on cbox (2.1 MB tree) and 4 on the dining proxy."""
+    auto takes 2 levels on cbox (2.1 MB tree) and the build's most (4 as
+    shipped) on the dining proxy."""
+    deep = _max_top_levels(rnd)
     for getter, camjson, depth, w, h, frames, auto in ((scenes.cbox_diffuse, scenes.CBOX_CAM, 8, 1024, 1024, 6, 2),
-                                                       (scenes.dining, scenes.DINING_CAM, 16, 1920, 1080, 2, 4)):
+                                                       (scenes.dining, scenes.DINING_CAM, 16, 1920, 1080, 2, deep)):
         data, cam = getter(), S.parse_camera(camjson)
         seeds = R.default_seeds(w * h)
         dsc = rnd.upload(data)
