@@ -2495,7 +2495,7 @@ int mcpt_render_frames(mcpt_ctx *ctx, const mcpt_scene *scene, const mcpt_camera
   const int depth_entries = p->mode == MCPT_MODE_NOPRUNE ? scene->stack_depth : scene->stack_depth4;
   A.lds_mats = scene->n_mats <= 256 ? 1 : 0;
   const size_t lds_mats = A.lds_mats ? scene->n_mats * sizeof(mcpt_material) : 0;
-  // persistent grid: as many 64-lane workgroups as can be resident at once.
+  // persistent grid: as many kWgWaves-wave workgroups as can be resident at once.
   // The stack lives in LDS; when the whole stack would allow fewer resident
   // workgroups than a kStackWindow window does, the windowed kernel runs.
   const bool noprune = p->mode == MCPT_MODE_NOPRUNE;
